@@ -1,0 +1,159 @@
+"""Pin the CPU oracle against the reference's own outputs (golden fixtures).
+
+Everything here runs on the CPU ("not gpu").  Bar: bit-exact.  The fixtures
+were produced by tools/gen_golden.py running /root/reference/astro itself."""
+import numpy as np
+import pytest
+
+from oracle import batched, mt19937, npsincos
+from tests import golden_io as gio
+
+CFG = gio.configs()
+
+
+# --------------------------------------------------------------------- KATs
+
+def test_kat_collisions():
+    # reference test_core.py:6-17 (as data)
+    k = gio.load_json('kat.json')['collisions']
+    assert batched.collisions_allpairs(k['x'], k['r']).tolist() == k['out'] == [False, True, True, True]
+
+
+def test_kat_direction_bits():
+    # util.direction (util.py:87-92) float32 output, bit for bit
+    k = gio.load_json('kat.json')
+    d = k['direction']
+    b = np.asarray(d['b'])
+    got = np.stack([npsincos.sin32(b.astype(np.float32)), npsincos.cos32(b.astype(np.float32))], -1)
+    np.testing.assert_allclose(got, d['out'], atol=1e-6)   # test_util.py:59-64
+    df = k['direction_f32']
+    b = np.asarray(df['b']).astype(np.float32)
+    got = np.stack([npsincos.sin32(b), npsincos.cos32(b)], -1)
+    assert (got.view(np.uint32) == np.asarray(df['out_bits'], dtype=np.uint32)).all()
+
+
+def test_npsincos_matches_numpy_exhaustive_sample():
+    rng = np.random.default_rng(7)
+    for scale in (1.0, 8.0, 300.0, 70000.0):
+        x = rng.uniform(-scale, scale, 400_000).astype(np.float32)
+        for mine, ref in ((npsincos.sin32, np.sin), (npsincos.cos32, np.cos)):
+            assert (mine(x).view(np.int32) == ref(x, dtype=np.float32).view(np.int32)).all()
+
+
+def test_kat_wrap():
+    k = gio.load_json('kat.json')
+    for key in ('wrap_unit_square', 'wrap_random'):
+        x = np.asarray(k[key]['x'])
+        got = batched._wrap(np.float64, x)
+        assert np.array_equal(got, np.asarray(k[key]['out']))
+
+
+# ----------------------------------------------------------- MT19937 / seeds
+
+def test_mt19937_words_match_numpy():
+    seeds = [0, 1, 42, 5489, 123456789, (1 << 31) + 7, (1 << 32) - 1]
+    w = mt19937.words(seeds, 1300)
+    for i, s in enumerate(seeds):
+        ref = np.random.RandomState(s).randint(0, 1 << 32, size=1300, dtype=np.uint64)
+        assert (w[i] == ref.astype(np.uint32)).all()
+
+
+def test_generate_configs_golden():
+    z = gio.load('generate_configs.npz')
+    for key in z.files:
+        seed = int(key.split('_', 1)[1])
+        assert (mt19937.generate_config_seeds(seed, 300) == z[key]).all()
+
+
+# ------------------------------------------------------------------ schedule
+
+def test_schedule_golden():
+    sched = gio.load_json('schedule.json')
+    for name, s in sched.items():
+        cfg = CFG['default']._replace(**s['config'])
+        fire, tt, ts, reloads = batched.schedule(cfg)
+        assert tt == s['timeout_tick'], name
+        assert np.nonzero(fire)[0].tolist() == s['fire_ticks'], name
+        assert ts[:50].tolist() == s['t'] and reloads[:50].tolist() == s['reload']
+        assert ts[-1] == s['t_last']
+
+
+# -------------------------------------------------------------------- create
+
+@pytest.mark.parametrize('name', sorted(CFG))
+def test_create_golden(name):
+    z = gio.load('create.npz')
+    cfg = CFG[name]
+    P = batched.make_params(cfg)
+    seeds = z[name + '__seed']
+    B = batched.create(seeds, P, p_pad=8, b_cap=4, store='f64')
+    S = P.nships
+    assert (B.nplanets == z[name + '__nplanets']).all()
+    assert np.array_equal(B.ships[..., 0:2].astype(np.float32), z[name + '__ships_x'][:, :S])
+    assert np.array_equal(B.ships[..., 2:4], z[name + '__ships_dx'][:, :S])
+    assert np.array_equal(B.ships_b.astype(np.float32), z[name + '__ships_b'][:, :S])
+    assert np.array_equal(B.planets[..., 0:2].astype(np.float32), z[name + '__planets_x'])
+    # planet velocities are float64 in the reference: compare the float64 values
+    assert np.array_equal(B.planets[..., 2:4], z[name + '__planets_dx'])
+    assert (B.nbullets == 0).all() and (B.tick == 0).all()
+
+
+# ------------------------------------------------- teacher-forced transitions
+
+def _compare(tag, got, rew, done, E, erew, edone):
+    assert (done == edone).all(), tag
+    assert np.array_equal(rew, erew.astype(np.float32)), tag
+    run = edone == 0
+    assert (got.nbullets[run] == E.nbullets[run]).all(), tag
+    assert np.array_equal(got.ships[run], E.ships[run]), tag
+    assert np.array_equal(got.ships_b[run], E.ships_b[run]), tag
+    pv = (np.arange(got.planets.shape[1])[None, :] < got.nplanets[:, None]) & run[:, None]
+    assert np.array_equal(got.planets[pv], E.planets[pv]), tag
+    bv = (np.arange(got.bullets.shape[1])[None, :] < got.nbullets[:, None]) & run[:, None]
+    assert np.array_equal(got.bullets[bv], E.bullets[bv]), tag
+
+
+@pytest.mark.parametrize('fname', ['steps.npz', 'edge_steps.npz'])
+def test_step_teacher_forced_bit_exact(fname):
+    """Oracle step (float64 arithmetic) == reference step on the same
+    (float32-valued) input states, bit for bit, including the tick-0 float32
+    paths, 1..8 planets, bullets, rewards and done causes."""
+    tr = gio.Transitions(fname)
+    total = 0
+    for name, idx in tr.groups():
+        cfg = CFG[name]
+        P = batched.make_params(cfg)
+        S = P.nships
+        B = tr.batch_in(idx, S)
+        got, rew, done = batched.step(B, tr.z['control'][idx], P, store='f64')
+        E, erew, edone = tr.expected(idx, S, b_cap=B.bullets.shape[1])
+        _compare('%s/%s' % (fname, name), got, rew, done, E, erew, edone)
+        total += idx.size
+    assert total == tr.n
+
+
+# ------------------------------------------------------- free-running games
+
+def test_games_free_running_float64_bit_exact():
+    """Whole games from create(seed) under the recorded open-loop controls:
+    the float64 oracle reproduces every ship state of every tick, the game
+    length, the bullet counts and the outcome."""
+    for g in gio.games():
+        cfg = CFG[g['cfg']]._replace(seed=int(g['seed']))
+        P = batched.make_params(cfg)
+        S = P.nships
+        st = batched.create([g['seed']], P, p_pad=8, b_cap=512, store='f64')
+        ticks = g['ships'].shape[0]
+        for t in range(ticks):
+            assert np.array_equal(st.ships[0], g['ships'][t, :S, 0:4]), (g['gid'], t)
+            assert np.array_equal(st.ships_b[0], g['ships'][t, :S, 4]), (g['gid'], t)
+            n = st.nplanets[0]
+            assert np.array_equal(st.planets[0, :n], g['planets'][t, :n]), (g['gid'], t)
+            assert st.nbullets[0] == g['nbullets'][t], (g['gid'], t)
+            ctl = np.zeros((1, 2), np.int64)
+            ctl[0, :S] = g['controls'][t]
+            st, rew, done = batched.step(st, ctl, P, store='f64')
+            if t < ticks - 1:
+                assert done[0] == 0
+        assert done[0] == g['done'], g['gid']
+        assert np.array_equal(rew[0], g['reward'][:S].astype(np.float32))
