@@ -1,0 +1,104 @@
+"""ctypes binding of libastro_hip.so (include/astro_step.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()``
+(hipcc --offload-arch=gfx950).  There is no fallback: if the library is
+missing or its ABI version differs, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
+ABI_VERSION = 1
+
+STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
+              'overflows', 'planets', 'reserved')
+NSTATS = 8
+
+
+class AstroParams(ctypes.Structure):
+    _fields_ = [
+        ('gm', ctypes.c_double),
+        ('dt', ctypes.c_double),
+        ('db', ctypes.c_double),
+        ('thrust', ctypes.c_double),
+        ('r2_ss', ctypes.c_double),
+        ('r2_sp', ctypes.c_double),
+        ('r2_s0', ctypes.c_double),
+        ('r2_p0', ctypes.c_double),
+        ('gravity', ctypes.c_double),
+        ('planet_mass', ctypes.c_double),
+        ('spawn_off', ctypes.c_float),
+        ('bullet_speed', ctypes.c_float),
+        ('timeout_reward', ctypes.c_float),
+        ('outer_pos', ctypes.c_float),
+        ('inner_pos', ctypes.c_float),
+        ('planet_orbit', ctypes.c_float),
+        ('nships', ctypes.c_int32),
+        ('solo', ctypes.c_int32),
+        ('max_planets', ctypes.c_int32),
+        ('p_pad', ctypes.c_int32),
+        ('b_cap', ctypes.c_int32),
+        ('timeout_tick', ctypes.c_int32),
+        ('fire_bits', ctypes.c_void_p),
+    ]
+
+
+class AstroState(ctypes.Structure):
+    _fields_ = [
+        ('ships', ctypes.c_void_p),
+        ('ships_b', ctypes.c_void_p),
+        ('planets', ctypes.c_void_p),
+        ('bullets', ctypes.c_void_p),
+        ('hdr', ctypes.c_void_p),
+        ('stream', ctypes.c_void_p),
+        ('n_env', ctypes.c_int32),
+        ('state_f64', ctypes.c_int32),
+    ]
+
+
+_SYMBOLS = {
+    'astro_abi_version': (ctypes.c_int, []),
+    'astro_last_error': (ctypes.c_char_p, []),
+    'astro_step': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    'astro_reset': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'astro_stream_init': (ctypes.c_int, [ctypes.POINTER(AstroState), ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+class AstroError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load (once) and type the library.  Raises if it is absent or stale."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise AstroError('%s is missing: build it with `python -c "import __graft_entry__ as g; '
+                         'g.build()"` (hipcc --offload-arch=gfx950)' % path)
+    # torch first: the library binds to the HIP runtime already in the process
+    import torch  # noqa: F401
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.astro_abi_version()
+    if v != ABI_VERSION:
+        raise AstroError('libastro_hip.so ABI %d != expected %d (rebuild)' % (v, ABI_VERSION))
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().astro_last_error().decode(errors='replace')
+        raise AstroError('%s failed (%d): %s' % (what, rc, msg))

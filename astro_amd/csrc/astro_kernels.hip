@@ -1,0 +1,786 @@
+// astro_kernels.hip -- MI355X (gfx950) batched lockstep Astro physics.
+//
+// One lane owns one game ("env"): a wave64 advances 64 independent games.
+// State is struct-of-arrays, entity-major ([slot][env]), so a wave's load of
+// slot s of its 64 envs is one contiguous 1 KiB (float) / 2 KiB (double)
+// stretch -- fully coalesced dwordx4 traffic, the only thing that matters for
+// an HBM-bound kernel.  No LDS: nothing is shared between envs, and each
+// lane's planets live in its own registers (there is no reuse across lanes
+// for LDS to capture).
+//
+// What is computed is exactly astro/core.py's step (core.py:215-303) and
+// create (core.py:86-135), including the reference's numpy dtype behaviour:
+//   * the first step of a game (tick 0) sees create()'s float32 arrays, so
+//     gravity, collision distances and tick-0 bullets run in float32;
+//   * every later step runs in float64 (numpy 2.x promotes the state);
+//   * a one-planet game keeps float32 planet arrays for ever;
+//   * util.direction (util.py:87-92) is numpy's own float32 sin/cos
+//     algorithm (np_sincosf below), so directions match numpy bit for bit.
+// The file is compiled with -ffp-contract=off: numpy never fuses a*b+c, and
+// neither may we, except where numpy's sin/cos itself uses an FMA.
+//
+// With float64 state the kernel therefore reproduces the reference bit for
+// bit; with float32 state every stored value is the float32 rounding of the
+// reference's value computed from the same (float32) input state.
+
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <type_traits>
+
+#include "astro_step.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// storage vectors (16-byte aligned; a D4 is two dwordx4)
+
+struct alignas(16) F4 { float x, y, z, w; };
+struct alignas(16) D4 { double x, y, z, w; };
+
+template <typename T> struct Store;
+template <> struct Store<float> { using V = F4; };
+template <> struct Store<double> { using V = D4; };
+
+// ---------------------------------------------------------------------------
+// numpy 2.x float32 sin/cos (loops_trigonometric.dispatch.cpp): Cody-Waite
+// reduction + minimax polynomials, every multiply-add fused as numpy's
+// MulAdd is.  Bit-exact to np.sin/np.cos(x, dtype=float32) for
+// |x| <= 71476.0625 (cos) / 117435.992 (sin); beyond, numpy falls back to
+// libm and so do we (ocml), which is the only place we may differ.  A game's
+// bearing changes by at most dt*ship_rspeed per tick, so it stays in range
+// for any max_time/dt below ~8.9e5 ticks at the default speed.
+
+__device__ __forceinline__ void np_sincosf(float x, float &s_out, float &c_out) {
+    const float two_over_pi = 0x1.45f306p-1f;
+    const float pio2_hi = -0x1.921fb0p+00f;
+    const float pio2_med = -0x1.5110b4p-22f;
+    const float pio2_lo = -0x1.846988p-48f;
+    const float magic = 0x1.800000p+23f;
+    float q = __builtin_fmaf(x, two_over_pi, magic) - magic;
+    float r = __builtin_fmaf(q, pio2_hi, x);
+    r = __builtin_fmaf(q, pio2_med, r);
+    r = __builtin_fmaf(q, pio2_lo, r);
+    float r2 = r * r;
+    float c = __builtin_fmaf(0x1.98e616p-16f, r2, -0x1.6c06dcp-10f);
+    c = __builtin_fmaf(c, r2, 0x1.55553cp-5f);
+    c = __builtin_fmaf(c, r2, -0x1.000000p-1f);
+    c = __builtin_fmaf(c, r2, 0x1.000000p+0f);
+    float s = __builtin_fmaf(0x1.7d3bbcp-19f, r2, -0x1.a06bbap-13f);
+    s = __builtin_fmaf(s, r2, 0x1.11119ap-07f);
+    s = __builtin_fmaf(s, r2, -0x1.555556p-03f);
+    s = __builtin_fmaf(s, r2, 0.0f);
+    s = __builtin_fmaf(s, r, r);
+    const int iq = (int)q;
+    float sv = (iq & 1) ? c : s;
+    if (iq & 2) sv = 0.0f - sv;
+    const int iq1 = iq + 1;
+    float cv = (iq1 & 1) ? c : s;
+    if (iq1 & 2) cv = 0.0f - cv;
+    const float ax = __builtin_fabsf(x);
+    if (ax > 117435.992f) sv = sinf(x);
+    if (ax > 71476.0625f) cv = cosf(x);
+    s_out = sv;
+    c_out = cv;
+}
+
+// util.wrap_unit_square (util.py:145-148): ((v + 1) % 2) - 1 with numpy's
+// floored remainder (npy_divmod: fmod, then +2 when negative, +0 when zero).
+template <typename C>
+__device__ __forceinline__ C wrap_unit(C v) {
+    C m = fmod(v + C(1), C(2));
+    if (m != C(0)) {
+        if (m < C(0)) m = m + C(2);
+    } else {
+        m = C(0);
+    }
+    return m - C(1);
+}
+
+// np.maximum(1e-12, d2): NaN-propagating max
+template <typename C>
+__device__ __forceinline__ C max_floor(C d2) {
+    const C k = C(1e-12);
+    return d2 < k ? k : d2;
+}
+
+// _gravity (core.py:138-153) at one point: sum over planets in index order,
+// field = gm / max(1e-12, |r|^2) * r  (a 1/r law in 2-D: no sqrt)
+template <typename C, int PMAX>
+__device__ __forceinline__ void field(const double (&px)[PMAX], const double (&py)[PMAX], int np,
+                                      double x, double y, double gm, C &gx, C &gy) {
+    C ax = C(0), ay = C(0);
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) {
+        if (j < np) {
+            const C rx = C(px[j]) - C(x);
+            const C ry = C(py[j]) - C(y);
+            const C d2 = rx * rx + ry * ry;
+            const C f = C(gm) / max_floor(d2);
+            const C tx = f * rx, ty = f * ry;
+            if (j == 0) {
+                ax = tx;
+                ay = ty;
+            } else {
+                ax = ax + tx;
+                ay = ay + ty;
+            }
+        }
+    }
+    gx = ax;
+    gy = ay;
+}
+
+// squared distance of _collisions (core.py:210) in precision C, compared in
+// float64 against the float64 (r_i + r_j)^2
+template <typename C>
+__device__ __forceinline__ double dist2(double ax, double ay, double bx, double by) {
+    const C dx = C(ax) - C(bx);
+    const C dy = C(ay) - C(by);
+    return double(dx * dx + dy * dy);
+}
+
+// ---------------------------------------------------------------------------
+// numpy legacy MT19937 (RandomState(int)), first 227 outputs, lazily: output
+// i needs init-key words i, i+1 and i+397 only, so two cursors over the
+// init_genrand recurrence replace the 624-word state (12 bytes, not 2.5 KB).
+
+__device__ __forceinline__ uint32_t mt_key_next(uint32_t prev, uint32_t idx) {
+    return 1812433253u * (prev ^ (prev >> 30)) + idx;
+}
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+struct MTLazy {
+    uint32_t a;  // key[i]
+    uint32_t b;  // key[i + 397]
+    uint32_t i;
+
+    __device__ void seed(uint32_t s) {
+        a = s;
+        uint32_t v = s;
+        for (uint32_t k = 1; k <= 397; ++k) v = mt_key_next(v, k);
+        b = v;
+        i = 0;
+    }
+    __device__ bool ok() const { return i < 227; }
+    __device__ uint32_t next() {
+        const uint32_t a1 = mt_key_next(a, i + 1);
+        const uint32_t y = (a & 0x80000000u) | (a1 & 0x7fffffffu);
+        const uint32_t tw = b ^ (y >> 1) ^ ((a1 & 1u) ? 0x9908b0dfu : 0u);
+        b = mt_key_next(b, i + 398);
+        a = a1;
+        ++i;
+        return mt_temper(tw);
+    }
+    // RandomState.rand(): 53-bit double from two words
+    __device__ double rand() {
+        const uint32_t hi = next() >> 5;
+        const uint32_t lo = next() >> 6;
+        return (double(hi) * 67108864.0 + double(lo)) / 9007199254740992.0;
+    }
+    // legacy RandomState.randint(lo, hi): masked rejection, nothing drawn
+    // for a single-value range
+    __device__ int randint(int lo, int hi) {
+        const uint32_t rng = uint32_t(hi - 1 - lo);
+        if (rng == 0) return lo;
+        uint32_t mask = rng;
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        mask |= mask >> 8;
+        mask |= mask >> 16;
+        uint32_t v;
+        do {
+            v = next() & mask;
+        } while (v > rng && ok());
+        return lo + int(v);
+    }
+};
+
+constexpr double TWO_PI = 6.283185307179586;  // 2 * np.pi
+constexpr double PI = 3.141592653589793;      // np.pi
+
+// ---------------------------------------------------------------------------
+// create() (core.py:86-135) for env i from `seed`; writes the env's slots.
+
+template <typename T, int S, int PMAX>
+__device__ void create_env(const AstroParams &p, const AstroState &st, int i, uint32_t seed,
+                           int &flags_out) {
+    using V = typename Store<T>::V;
+    const size_t N = size_t(st.n_env);
+    V *ships = reinterpret_cast<V *>(st.ships);
+    T *ships_b = reinterpret_cast<T *>(st.ships_b);
+    V *planets = reinterpret_cast<V *>(st.planets);
+
+    MTLazy g;
+    g.seed(seed);
+    int n = g.randint(1, p.max_planets + 1);
+    // outer = outer_ship_position * sign(rand(2).astype(float32) - 0.5)
+    const float u0 = float(g.rand()) - 0.5f;
+    const float u1 = float(g.rand()) - 0.5f;
+    const float o0 = p.outer_pos * (u0 > 0.0f ? 1.0f : (u0 < 0.0f ? -1.0f : 0.0f));
+    const float o1 = p.outer_pos * (u1 > 0.0f ? 1.0f : (u1 < 0.0f ? -1.0f : 0.0f));
+    // inner = inner_ship_position * direction(2 pi rand())
+    float is, ic;
+    np_sincosf(float(TWO_PI * g.rand()), is, ic);
+    const float i0 = p.inner_pos * is, i1 = p.inner_pos * ic;
+    float shx[2], shy[2];
+    if (n == 1) {
+        shx[0] = o0;
+        shy[0] = o1;
+        shx[1] = -o0;
+        shy[1] = -o1;
+    } else if (S == 1) {
+        const bool outer = g.rand() < 0.5;
+        shx[0] = outer ? o0 : i0;
+        shy[0] = outer ? o1 : i1;
+        shx[1] = shy[1] = 0.0f;
+    } else {
+        const bool outer_first = g.rand() < 0.5;
+        shx[0] = outer_first ? o0 : i0;
+        shy[0] = outer_first ? o1 : i1;
+        shx[1] = outer_first ? i0 : o0;
+        shy[1] = outer_first ? i1 : o1;
+    }
+    // b = 2 pi * rand(S).astype(float32)   (float32 product)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const float b = 6.2831855f * float(g.rand());
+        V v;
+        v.x = T(shx[s]);
+        v.y = T(shy[s]);
+        v.z = T(0);
+        v.w = T(0);
+        ships[size_t(s) * N + i] = v;
+        ships_b[size_t(s) * N + i] = T(b);
+    }
+    if (n == 1) {
+        V v;
+        v.x = v.y = v.z = v.w = T(0);
+        planets[i] = v;
+    } else {
+        const double base = TWO_PI * g.rand();
+        const double stp = TWO_PI / double(n);
+        const int reverse = g.randint(0, 2) == 0 ? -1 : 1;
+        const double amp = sqrt(p.gravity * p.planet_mass * double(n - 1) / 2.0);
+        const double turn = double(reverse) * PI / 2.0;
+        for (int j = 0; j < n && j < PMAX; ++j) {
+            const double orient = base + double(j) * stp;
+            float ps, pc, vs, vc;
+            np_sincosf(float(orient), ps, pc);
+            np_sincosf(float(orient + turn), vs, vc);
+            V v;
+            v.x = T(p.planet_orbit * ps);
+            v.y = T(p.planet_orbit * pc);
+            v.z = T(amp * double(vs));
+            v.w = T(amp * double(vc));
+            planets[size_t(j) * N + i] = v;
+        }
+    }
+    if (n > PMAX) n = PMAX;
+    flags_out = g.ok() ? 0 : 2;
+    st.hdr[2 * i + 0] = 0;
+    st.hdr[2 * i + 1] = n;
+}
+
+// next config seed of env i's generate_configs stream (core.py:77-83):
+// RandomState(stream_seed).randint(1 << 30) = one masked MT word per game
+__device__ __forceinline__ uint32_t stream_next(const AstroState &st, int i, bool &exhausted) {
+    uint4 c = reinterpret_cast<uint4 *>(st.stream)[i];
+    MTLazy g;
+    g.a = c.x;
+    g.b = c.y;
+    g.i = c.z;
+    exhausted = !g.ok();
+    const uint32_t seed = g.next() & ((1u << 30) - 1);
+    c.x = g.a;
+    c.y = g.b;
+    c.z = g.i;
+    c.w = seed;
+    reinterpret_cast<uint4 *>(st.stream)[i] = c;
+    return seed;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// the step kernel
+
+constexpr int BLOCK = 64;
+constexpr int BCHUNK = 8;  // bullets loaded per batch: 8 loads in flight per lane
+
+template <typename T, int S, int PMAX>
+__global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroState st,
+                                                           const int8_t *__restrict__ control,
+                                                           float *__restrict__ reward,
+                                                           uint8_t *__restrict__ done_out,
+                                                           unsigned long long *stats,
+                                                           int auto_reset) {
+    using V = typename Store<T>::V;
+    const int N = st.n_env;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool active = i < N;
+    uint64_t st_bin = 0, st_bout = 0, st_reset = 0, st_coll = 0, st_tout = 0, st_ovf = 0, st_pl = 0;
+
+    if (active) {
+        const size_t NN = size_t(N);
+        V *ships = reinterpret_cast<V *>(st.ships);
+        T *ships_b = reinterpret_cast<T *>(st.ships_b);
+        V *planets = reinterpret_cast<V *>(st.planets);
+        V *bullets = reinterpret_cast<V *>(st.bullets);
+
+        const int2 h = reinterpret_cast<const int2 *>(st.hdr)[i];
+        const int tick = h.x;
+        int np = h.y & 0xff;
+        int flags = (h.y >> 8) & 0xff;
+        const int nb = int(uint32_t(h.y) >> 16);
+        np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+
+        // ---- loads: ships, planets (padded slots re-read slot 0), control
+        double sx[S], sy[S], sdx[S], sdy[S], sb[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const V v = ships[size_t(s) * NN + i];
+            sx[s] = double(v.x);
+            sy[s] = double(v.y);
+            sdx[s] = double(v.z);
+            sdy[s] = double(v.w);
+            sb[s] = double(ships_b[size_t(s) * NN + i]);
+        }
+        double px[PMAX], py[PMAX], pdx[PMAX], pdy[PMAX];
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+            const int jj = j < np ? j : 0;
+            const V v = planets[size_t(jj) * NN + i];
+            px[j] = double(v.x);
+            py[j] = double(v.y);
+            pdx[j] = double(v.z);
+            pdy[j] = double(v.w);
+        }
+        int ctl[S];
+        if (S == 2) {
+            const uint16_t c2 = reinterpret_cast<const uint16_t *>(control)[i];
+            ctl[0] = int(int8_t(c2 & 0xff));
+            ctl[S - 1] = int(int8_t(c2 >> 8));
+        } else {
+            ctl[0] = int(control[i]);
+        }
+        st_pl = uint64_t(np);
+
+        const bool t0 = tick == 0;
+
+        // ---- ship acceleration (core.py:234-239): thrust along direction(b)
+        //      + gravity; floor //2 and %2 of the control code
+        float ds[S], dc[S];
+        double ax[S], ay[S], dbear[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            np_sincosf(float(sb[s]), ds[s], dc[s]);
+            double gx, gy;
+            if (t0) {
+                float fx, fy;
+                field<float, PMAX>(px, py, np, sx[s], sy[s], p.gm, fx, fy);
+                gx = double(fx);
+                gy = double(fy);
+            } else {
+                field<double, PMAX>(px, py, np, sx[s], sy[s], p.gm, gx, gy);
+            }
+            const double thr = p.thrust * double(ctl[s] & 1);
+            ax[s] = thr * double(ds[s]) + gx;
+            ay[s] = thr * double(dc[s]) + gy;
+            dbear[s] = p.db * double((ctl[s] >> 1) - 1);
+        }
+
+        // ---- collisions on the old state (core.py:241-253): ships vs
+        //      ships/planets here, ships/planets vs bullets in the bullet pass
+        bool hit[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            bool hs = false;
+#pragma unroll
+            for (int j = 0; j < PMAX; ++j) {
+                if (j < np) {
+                    const double d2 = t0 ? dist2<float>(sx[s], sy[s], px[j], py[j])
+                                         : dist2<double>(sx[s], sy[s], px[j], py[j]);
+                    hs = hs || d2 < p.r2_sp;
+                }
+            }
+            hit[s] = hs;
+        }
+        if (S == 2) {
+            const double d2 = t0 ? dist2<float>(sx[0], sy[0], sx[S - 1], sy[S - 1])
+                                 : dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]);
+            const bool hh = d2 < p.r2_ss;
+            hit[0] = hit[0] || hh;
+            hit[S - 1] = hit[S - 1] || hh;
+        }
+
+        // ---- bullet pass: collide (old positions), then survivors move
+        //      without gravity and are culled when both coords leave [-1, 1]
+        //      (core.py:264-266, 295-300, 195), compacted in order in place
+        const bool live = tick < p.timeout_tick;
+        const bool fire = live && ((p.fire_bits[tick >> 5] >> (tick & 31)) & 1u);
+        int w = 0;         // bullets written
+        int dropped = 0;   // bullets lost to b_cap
+        const int bcap = p.b_cap;
+
+        auto emit = [&](double x, double y, double dx, double dy) {
+            if (w < bcap) {
+                V v;
+                v.x = T(x);
+                v.y = T(y);
+                v.z = T(dx);
+                v.w = T(dy);
+                bullets[size_t(w) * NN + i] = v;
+                ++w;
+            } else {
+                ++dropped;
+            }
+        };
+        // one bullet: returns nothing, updates hit[] and emits the survivor
+        auto bullet = [&](const V &v) {
+            const double x = double(v.x), y = double(v.y), dx = double(v.z), dy = double(v.w);
+            bool bh = false;
+#pragma unroll
+            for (int j = 0; j < PMAX; ++j) {
+                if (j < np) {
+                    const double d2 = t0 ? dist2<float>(x, y, px[j], py[j])
+                                         : dist2<double>(x, y, px[j], py[j]);
+                    bh = bh || d2 < p.r2_p0;
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const double d2 = t0 ? dist2<float>(x, y, sx[s], sy[s]) : dist2<double>(x, y, sx[s], sy[s]);
+                const bool hs = d2 < p.r2_s0;
+                bh = bh || hs;
+                hit[s] = hit[s] || hs;
+            }
+            if (!bh) {
+                if (t0) {
+                    const float ndx = float(dx) + 0.0f, ndy = float(dy) + 0.0f;
+                    const float dtf = float(p.dt);
+                    const float nx = float(x) + dtf * ndx, ny = float(y) + dtf * ndy;
+                    if ((-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f)) emit(nx, ny, ndx, ndy);
+                } else {
+                    const double ndx = dx + 0.0, ndy = dy + 0.0;
+                    const double nx = x + p.dt * ndx, ny = y + p.dt * ndy;
+                    if ((-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0)) emit(nx, ny, ndx, ndy);
+                }
+            }
+        };
+        for (int base = 0; base < nb; base += BCHUNK) {
+            V buf[BCHUNK];
+#pragma unroll
+            for (int u = 0; u < BCHUNK; ++u) {
+                const int k = base + u < nb ? base + u : 0;
+                buf[u] = bullets[size_t(k) * NN + i];
+            }
+#pragma unroll
+            for (int u = 0; u < BCHUNK; ++u)
+                if (base + u < nb) bullet(buf[u]);
+        }
+        st_bin = uint64_t(nb);
+
+        const bool collided = S == 2 ? (hit[0] || hit[S - 1]) : hit[0];
+        const bool timeout = !collided && !live;
+        const uint8_t done = collided ? 1 : (timeout ? 2 : 0);
+
+        // rewards (core.py:253-260)
+        float rw[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            rw[s] = collided ? (hit[s] ? -1.0f : 1.0f) : (timeout ? p.timeout_reward : 0.0f);
+        if (S == 2) {
+            reinterpret_cast<float2 *>(reward)[i] = make_float2(rw[0], rw[S - 1]);
+        } else {
+            reward[i] = rw[0];
+        }
+        done_out[i] = done;
+
+        if (!done) {
+            // ---- fire: one new bullet per ship from the OLD ship state,
+            //      appended after the survivors (core.py:267-280)
+            if (fire) {
+                const float dtf = float(p.dt);
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const float os = p.spawn_off * ds[s], oc = p.spawn_off * dc[s];
+                    const float vs = p.bullet_speed * ds[s], vc = p.bullet_speed * dc[s];
+                    if (t0) {
+                        const float bx = float(sx[s]) + os, by = float(sy[s]) + oc;
+                        const float bdx = float(sdx[s]) + vs + 0.0f, bdy = float(sdy[s]) + vc + 0.0f;
+                        const float nx = bx + dtf * bdx, ny = by + dtf * bdy;
+                        if ((-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f)) emit(nx, ny, bdx, bdy);
+                    } else {
+                        const double bx = sx[s] + double(os), by = sy[s] + double(oc);
+                        const double bdx = (sdx[s] + double(vs)) + 0.0, bdy = (sdy[s] + double(vc)) + 0.0;
+                        const double nx = bx + p.dt * bdx, ny = by + p.dt * bdy;
+                        if ((-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0)) emit(nx, ny, bdx, bdy);
+                    }
+                }
+            }
+
+            // ---- ships: semi-implicit Euler, wrap (core.py:283-288, 189-197)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const double ndx = sdx[s] + ax[s] * p.dt;
+                const double ndy = sdy[s] + ay[s] * p.dt;
+                V v;
+                v.x = T(wrap_unit<double>(sx[s] + p.dt * ndx));
+                v.y = T(wrap_unit<double>(sy[s] + p.dt * ndy));
+                v.z = T(ndx);
+                v.w = T(ndy);
+                ships[size_t(s) * NN + i] = v;
+                ships_b[size_t(s) * NN + i] = T(sb[s] + dbear[s]);
+            }
+
+            // ---- planets: mutual gravity incl. the (zero) self term
+            //      (core.py:289-294); float32 at tick 0 / for a lone planet
+            const float dtf = float(p.dt);
+#pragma unroll
+            for (int j = 0; j < PMAX; ++j) {
+                if (j < np) {
+                    V v;
+                    if (np == 1) {
+                        float gx, gy;
+                        field<float, PMAX>(px, py, np, px[j], py[j], p.gm, gx, gy);
+                        const float ndx = float(pdx[j]) + gx * dtf;
+                        const float ndy = float(pdy[j]) + gy * dtf;
+                        v.x = T(wrap_unit<float>(float(px[j]) + dtf * ndx));
+                        v.y = T(wrap_unit<float>(float(py[j]) + dtf * ndy));
+                        v.z = T(ndx);
+                        v.w = T(ndy);
+                    } else {
+                        double ndx, ndy;
+                        if (t0) {
+                            float gx, gy;
+                            field<float, PMAX>(px, py, np, px[j], py[j], p.gm, gx, gy);
+                            ndx = pdx[j] + double(gx * dtf);
+                            ndy = pdy[j] + double(gy * dtf);
+                        } else {
+                            double gx, gy;
+                            field<double, PMAX>(px, py, np, px[j], py[j], p.gm, gx, gy);
+                            ndx = pdx[j] + gx * p.dt;
+                            ndy = pdy[j] + gy * p.dt;
+                        }
+                        v.x = T(wrap_unit<double>(px[j] + p.dt * ndx));
+                        v.y = T(wrap_unit<double>(py[j] + p.dt * ndy));
+                        v.z = T(ndx);
+                        v.w = T(ndy);
+                    }
+                    planets[size_t(j) * NN + i] = v;
+                }
+            }
+            if (dropped) flags |= 1;
+            reinterpret_cast<int2 *>(st.hdr)[i] = make_int2(tick + 1, np | (flags << 8) | (w << 16));
+            st_bout = uint64_t(w);
+            st_ovf = uint64_t(dropped);
+        } else {
+            st_coll = collided ? 1 : 0;
+            st_tout = timeout ? 1 : 0;
+            if (auto_reset) {
+                bool exhausted;
+                const uint32_t seed = stream_next(st, i, exhausted);
+                int cf = 0;
+                create_env<T, S, PMAX>(p, st, i, seed, cf);
+                if (exhausted || cf) st.hdr[2 * i + 1] |= 2 << 8;
+                st_reset = 1;
+            }
+        }
+    }
+
+    if (stats) {
+        const uint64_t a = wave_sum(st_bin), b = wave_sum(st_bout), c = wave_sum(st_reset);
+        const uint64_t d = wave_sum(st_coll), e = wave_sum(st_tout), f = wave_sum(st_ovf);
+        const uint64_t g = wave_sum(st_pl);
+        if ((threadIdx.x & 63) == 0) {
+            if (a) atomicAdd(stats + ASTRO_STAT_BULLETS_IN, (unsigned long long)a);
+            if (b) atomicAdd(stats + ASTRO_STAT_BULLETS_OUT, (unsigned long long)b);
+            if (c) atomicAdd(stats + ASTRO_STAT_RESETS, (unsigned long long)c);
+            if (d) atomicAdd(stats + ASTRO_STAT_COLLISIONS, (unsigned long long)d);
+            if (e) atomicAdd(stats + ASTRO_STAT_TIMEOUTS, (unsigned long long)e);
+            if (f) atomicAdd(stats + ASTRO_STAT_OVERFLOWS, (unsigned long long)f);
+            if (g) atomicAdd(stats + ASTRO_STAT_PLANETS, (unsigned long long)g);
+        }
+    }
+}
+
+template <typename T, int S, int PMAX>
+__global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, AstroState st,
+                                                            const uint32_t *__restrict__ seeds,
+                                                            const uint8_t *__restrict__ mask) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= st.n_env) return;
+    if (mask && !mask[i]) return;
+    bool exhausted = false;
+    const uint32_t seed = seeds ? seeds[i] : stream_next(st, i, exhausted);
+    int cf = 0;
+    create_env<T, S, PMAX>(p, st, i, seed, cf);
+    if (exhausted || cf) st.hdr[2 * i + 1] |= 2 << 8;
+    if (seeds && st.stream) reinterpret_cast<uint32_t *>(st.stream)[4 * i + 3] = seed;
+}
+
+__global__ __launch_bounds__(BLOCK) void astro_stream_init_kernel(AstroState st,
+                                                                  const uint32_t *__restrict__ seeds) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= st.n_env) return;
+    MTLazy g;
+    g.seed(seeds[i]);
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, 0u);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+int check_state(const AstroState *s) {
+    if (!s) return fail(-2, "state is NULL");
+    if (s->n_env < 0) return fail(-3, "n_env < 0");
+    if (s->n_env == 0) return 0;
+    if (!s->ships || !s->ships_b || !s->planets || !s->bullets || !s->hdr)
+        return fail(-4, "a state array is NULL");
+    if (!aligned16(s->ships) || !aligned16(s->planets) || !aligned16(s->bullets))
+        return fail(-5, "ships/planets/bullets must be 16-byte aligned");
+    if ((reinterpret_cast<uintptr_t>(s->hdr) & 7u) != 0) return fail(-5, "hdr must be 8-byte aligned");
+    if (s->state_f64 != 0 && s->state_f64 != 1) return fail(-6, "state_f64 must be 0 or 1");
+    return 0;
+}
+
+int check_params(const AstroParams *p) {
+    if (!p) return fail(-10, "params is NULL");
+    if (p->nships != 1 && p->nships != 2) return fail(-11, "nships must be 1 or 2");
+    if (p->nships != (p->solo ? 1 : 2)) return fail(-12, "nships must be 1 iff solo");
+    if (p->p_pad < 1 || p->p_pad > 16) return fail(-13, "p_pad must be in [1, 16]");
+    if (p->max_planets < 1 || p->max_planets > p->p_pad)
+        return fail(-14, "max_planets must be in [1, p_pad]");
+    if (p->b_cap < 1 || p->b_cap > 65535) return fail(-15, "b_cap must be in [1, 65535]");
+    if (p->timeout_tick < 0) return fail(-16, "timeout_tick < 0");
+    if (p->timeout_tick > 0 && !p->fire_bits) return fail(-17, "fire_bits is NULL");
+    return 0;
+}
+
+int launched(const char *what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(-1000 - int(e), "%s launch failed: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
+template <typename T, int S, int PM>
+int launch_step(const AstroParams &p, const AstroState &s, const int8_t *c, float *r, uint8_t *d,
+                uint64_t *stats, int ar, hipStream_t stream) {
+    const int grid = (s.n_env + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL((astro_step_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, c, r, d,
+                       reinterpret_cast<unsigned long long *>(stats), ar);
+    return launched("astro_step");
+}
+
+template <typename T, int S, int PM>
+int launch_reset(const AstroParams &p, const AstroState &s, const uint32_t *seeds, const uint8_t *mask,
+                 hipStream_t stream) {
+    const int grid = (s.n_env + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL((astro_reset_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, seeds, mask);
+    return launched("astro_reset");
+}
+
+// dispatch over (storage type, ships, planet register capacity)
+template <template <typename, int, int> class L, typename... A>
+int dispatch(const AstroParams &p, const AstroState &s, A... a) {
+    const int pm = p.p_pad <= 4 ? 4 : (p.p_pad <= 8 ? 8 : 16);
+#define ASTRO_CASE(T, S, PM) \
+    if (std::is_same<T, double>::value == bool(s.state_f64) && p.nships == S && pm == PM) \
+        return L<T, S, PM>::run(p, s, a...);
+    ASTRO_CASE(float, 1, 4) ASTRO_CASE(float, 1, 8) ASTRO_CASE(float, 1, 16)
+    ASTRO_CASE(float, 2, 4) ASTRO_CASE(float, 2, 8) ASTRO_CASE(float, 2, 16)
+    ASTRO_CASE(double, 1, 4) ASTRO_CASE(double, 1, 8) ASTRO_CASE(double, 1, 16)
+    ASTRO_CASE(double, 2, 4) ASTRO_CASE(double, 2, 8) ASTRO_CASE(double, 2, 16)
+#undef ASTRO_CASE
+    return fail(-20, "no kernel instance for this configuration");
+}
+
+template <typename T, int S, int PM>
+struct StepL {
+    static int run(const AstroParams &p, const AstroState &s, const int8_t *c, float *r, uint8_t *d,
+                   uint64_t *stats, int ar, hipStream_t st) {
+        return launch_step<T, S, PM>(p, s, c, r, d, stats, ar, st);
+    }
+};
+template <typename T, int S, int PM>
+struct ResetL {
+    static int run(const AstroParams &p, const AstroState &s, const uint32_t *seeds, const uint8_t *mask,
+                   hipStream_t st) {
+        return launch_reset<T, S, PM>(p, s, seeds, mask, st);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int astro_abi_version(void) { return ASTRO_ABI_VERSION; }
+
+const char *astro_last_error(void) { return g_err; }
+
+int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control, float *reward,
+               uint8_t *done, uint64_t *stats, int32_t auto_reset, void *stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if ((rc = check_state(s))) return rc;
+    if (s->n_env == 0) return 0;
+    if (!control || !reward || !done) return fail(-30, "control/reward/done is NULL");
+    if (auto_reset && !s->stream) return fail(-31, "auto_reset needs the stream array");
+    if (p->nships == 2 && ((reinterpret_cast<uintptr_t>(control) & 1u) || (reinterpret_cast<uintptr_t>(reward) & 7u)))
+        return fail(-32, "control must be 2-byte and reward 8-byte aligned");
+    if (stats && (reinterpret_cast<uintptr_t>(stats) & 7u)) return fail(-33, "stats must be 8-byte aligned");
+    return dispatch<StepL>(*p, *s, control, reward, done, stats, int(auto_reset),
+                           reinterpret_cast<hipStream_t>(stream));
+}
+
+int astro_reset(const AstroParams *p, const AstroState *s, const uint32_t *seeds, const uint8_t *mask,
+                void *stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if ((rc = check_state(s))) return rc;
+    if (s->n_env == 0) return 0;
+    if (!seeds && !s->stream) return fail(-40, "reset without seeds needs the stream array");
+    return dispatch<ResetL>(*p, *s, seeds, mask, reinterpret_cast<hipStream_t>(stream));
+}
+
+int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *stream) {
+    if (!s) return fail(-2, "state is NULL");
+    if (s->n_env < 0) return fail(-3, "n_env < 0");
+    if (s->n_env == 0) return 0;
+    if (!s->stream || !stream_seeds) return fail(-41, "stream / stream_seeds is NULL");
+    if (reinterpret_cast<uintptr_t>(s->stream) & 15u) return fail(-5, "stream must be 16-byte aligned");
+    const int grid = (s->n_env + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(astro_stream_init_kernel, dim3(grid), dim3(BLOCK), 0,
+                       reinterpret_cast<hipStream_t>(stream), *s, stream_seeds);
+    return launched("astro_stream_init");
+}
+
+}  // extern "C"

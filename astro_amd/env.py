@@ -1,0 +1,239 @@
+"""BatchedEnv: N independent Astro games advanced in lockstep on one GPU.
+
+This is the batched counterpart of the reference's per-game loop
+(``core.play``, core.py:377-410 driving ``core.step``/``core.create``):
+``reset()`` creates every game, ``step(control)`` advances every game by one
+tick and, for games that end, starts the env's next game in the same kernel
+(auto-reset).  Env i plays the games of
+``generate_configs(config._replace(seed=stream_seed[i]))`` where
+``stream_seed`` = the first configs of ``generate_configs(config)``
+(core.py:77-83), indexed by GLOBAL env id, so a run sharded over G GPUs
+(``env_offset``) plays exactly the games of a 1-GPU run.
+
+All state lives in HBM as PyTorch tensors, struct-of-arrays, entity-major:
+
+    ships    [S, N, 4]   x, y, dx, dy        ships_b  [S, N]
+    planets  [P, N, 4]   x, y, dx, dy        bullets  [B, N, 4]
+    hdr      [N, 2]      tick, nplanets | flags << 8 | nbullets << 16
+    stream   [N, 4]      seed-stream cursor + current game seed
+
+and every call goes through libastro_hip.so (include/astro_step.h) on the
+current torch stream.  There is no CPU path.
+"""
+import collections
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import Bodies, State, nships as _nships
+from . import schedule as _schedule
+
+Observation = collections.namedtuple(
+    'Observation', ('ships', 'ships_b', 'planets', 'nplanets', 'bullets', 'nbullets', 'tick'))
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class BatchedEnv:
+    """N lockstep games of one Config on one device.
+
+    config     -- astro_amd.Config (same fields as astro.core.Config)
+    n_env      -- envs on this device
+    b_cap      -- bullet slots per env (bullets beyond are dropped and
+                  counted: hdr flag bit0 + stats 'overflows')
+    p_pad      -- planet slots per env (default: config.max_planets)
+    dtype      -- torch.float32 (default) or torch.float64 state storage
+    env_offset -- global id of env 0 (multi-GPU sharding)
+    """
+
+    def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
+                 dtype=torch.float32, env_offset=0, auto_reset=True):
+        _schedule.check_config(config)
+        if dtype not in (torch.float32, torch.float64):
+            raise ValueError('dtype must be torch.float32 or torch.float64')
+        self.lib = _lib.load()
+        self.config = config
+        self.n_env = int(n_env)
+        self.S = _nships(config)
+        self.p_pad = int(p_pad or config.max_planets)
+        if self.p_pad < config.max_planets or self.p_pad > 16:
+            raise ValueError('p_pad must be in [max_planets, 16]')
+        self.b_cap = int(b_cap)
+        self.dtype = dtype
+        self.device = torch.device(device if device is not None else 'cuda')
+        if self.device.type != 'cuda':
+            raise ValueError('BatchedEnv runs on a HIP device only (got %s)' % self.device)
+        self.env_offset = int(env_offset)
+        self.auto_reset = bool(auto_reset)
+        self.schedule = _schedule.build(config)
+
+        N, S, dev = self.n_env, self.S, self.device
+        z = lambda *shape, dt=dtype: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
+        self.ships = z(S, N, 4)
+        self.ships_b = z(S, N)
+        self.planets = z(self.p_pad, N, 4)
+        self.bullets = z(self.b_cap, N, 4)
+        self.hdr = z(N, 2, dt=torch.int32)
+        self.stream = z(N, 4, dt=torch.int32)
+        self.reward = z(N, S, dt=torch.float32)
+        self.done = z(N, dt=torch.uint8)
+        self.stats = z(_lib.NSTATS, dt=torch.int64)
+        self.fire_bits = torch.from_numpy(self.schedule.fire_bits().view(np.int32)).to(dev)
+
+        k = _schedule.kernel_constants(config)
+        self.params = _lib.AstroParams(
+            p_pad=self.p_pad, b_cap=self.b_cap, timeout_tick=self.schedule.timeout_tick,
+            fire_bits=self.fire_bits.data_ptr(), **k)
+        self.state = _lib.AstroState(
+            ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),
+            planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),
+            hdr=self.hdr.data_ptr(), stream=self.stream.data_ptr(),
+            n_env=N, state_f64=1 if dtype == torch.float64 else 0)
+
+        seeds = np.random.RandomState(config.seed).randint(
+            1 << 30, size=self.env_offset + N)[self.env_offset:]
+        self.stream_seeds = seeds.astype(np.uint32)
+        seeds_t = torch.from_numpy(self.stream_seeds.view(np.int32)).to(dev)
+        _lib.check(self.lib.astro_stream_init(ctypes.byref(self.state), seeds_t.data_ptr(),
+                                              _stream_ptr(dev)), 'astro_stream_init')
+        torch.cuda.current_stream(dev).synchronize()
+
+    # ------------------------------------------------------------------ calls
+
+    def reset(self, mask=None, seeds=None):
+        """core.create for every env (or those with mask != 0): from the next
+        seed of each env's stream, or from explicit ``seeds`` (uint32 [N])."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        s = None
+        if seeds is not None:
+            s = torch.as_tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32)
+                                if not torch.is_tensor(seeds) else seeds,
+                                device=self.device).to(torch.int32).contiguous()
+        _lib.check(self.lib.astro_reset(
+            ctypes.byref(self.params), ctypes.byref(self.state),
+            None if s is None else s.data_ptr(), None if m is None else m.data_ptr(),
+            _stream_ptr(self.device)), 'astro_reset')
+        self._keep = (m, s)   # keep the arguments alive until the call has run
+        return self.obs()
+
+    def step(self, control, auto_reset=None, stats=True):
+        """core.step for every env.  control: int8 [N, S] device tensor (or
+        anything torch.as_tensor accepts).  Returns (obs, reward f32 [N, S],
+        done u8 [N]); done = 1 ship collision, 2 timeout.  Finished envs are
+        re-created in the same launch when auto_reset is on."""
+        c = control
+        if not (torch.is_tensor(c) and c.dtype == torch.int8 and c.device == self.device
+                and c.is_contiguous()):
+            c = torch.as_tensor(c, device=self.device).to(torch.int8).contiguous()
+        if c.shape != (self.n_env, self.S):
+            raise ValueError('control must be [%d, %d], got %s' % (self.n_env, self.S, tuple(c.shape)))
+        self.launch(c.data_ptr(), auto_reset, stats)
+        self._ctl = c
+        return self.obs(), self.reward, self.done
+
+    def launch(self, control_ptr, auto_reset=None, stats=True, stream=None):
+        """Raw launch (no checks, no allocation): for timed loops/graphs."""
+        ar = self.auto_reset if auto_reset is None else bool(auto_reset)
+        rc = self.lib.astro_step(
+            ctypes.byref(self.params), ctypes.byref(self.state), control_ptr,
+            self.reward.data_ptr(), self.done.data_ptr(),
+            self.stats.data_ptr() if stats else None, 1 if ar else 0,
+            stream if stream is not None else _stream_ptr(self.device))
+        if rc != 0:
+            _lib.check(rc, 'astro_step')
+
+    # ------------------------------------------------------------ observation
+
+    @property
+    def tick(self):
+        return self.hdr[:, 0]
+
+    @property
+    def nplanets(self):
+        return self.hdr[:, 1] & 0xff
+
+    @property
+    def flags(self):
+        return (self.hdr[:, 1] >> 8) & 0xff
+
+    @property
+    def nbullets(self):
+        return (self.hdr[:, 1] >> 16) & 0xffff
+
+    @property
+    def game_seed(self):
+        return self.stream[:, 3]
+
+    def obs(self):
+        """Env-major views of the state (no copies): ships [N, S, 4] ..."""
+        return Observation(
+            ships=self.ships.permute(1, 0, 2), ships_b=self.ships_b.permute(1, 0),
+            planets=self.planets.permute(1, 0, 2), nplanets=self.nplanets,
+            bullets=self.bullets.permute(1, 0, 2), nbullets=self.nbullets, tick=self.tick)
+
+    def stat_dict(self):
+        v = self.stats.cpu().tolist()
+        return dict(zip(_lib.STAT_NAMES, v))
+
+    # ----------------------------------------------------- host import/export
+
+    def to_host(self):
+        """Every array as numpy (synchronises)."""
+        return dict(ships=self.ships.permute(1, 0, 2).cpu().numpy(),
+                    ships_b=self.ships_b.permute(1, 0).cpu().numpy(),
+                    planets=self.planets.permute(1, 0, 2).cpu().numpy(),
+                    bullets=self.bullets.permute(1, 0, 2).cpu().numpy(),
+                    tick=self.tick.cpu().numpy(), nplanets=self.nplanets.cpu().numpy(),
+                    nbullets=self.nbullets.cpu().numpy(), flags=self.flags.cpu().numpy())
+
+    def load_host(self, ships, ships_b, planets, bullets, tick, nplanets, nbullets):
+        """Overwrite the state from host arrays (env-major, like to_host)."""
+        dev, dt = self.device, self.dtype
+
+        def put(dst, src):
+            dst.copy_(torch.as_tensor(np.ascontiguousarray(src)).to(dt))
+        put(self.ships, np.asarray(ships).transpose(1, 0, 2))
+        put(self.ships_b, np.asarray(ships_b).transpose(1, 0))
+        pl = np.zeros((self.n_env, self.p_pad, 4))
+        pl[:, :np.asarray(planets).shape[1]] = planets
+        put(self.planets, pl.transpose(1, 0, 2))
+        bl = np.zeros((self.n_env, self.b_cap, 4))
+        bsrc = np.asarray(bullets)
+        nbmax = min(bsrc.shape[1], self.b_cap)
+        bl[:, :nbmax] = bsrc[:, :nbmax]
+        put(self.bullets, bl.transpose(1, 0, 2))
+        nb = np.asarray(nbullets, dtype=np.int64)
+        if (nb > self.b_cap).any():
+            raise ValueError('a state holds more bullets than b_cap')
+        hdr = np.stack([np.asarray(tick, np.int64),
+                        np.asarray(nplanets, np.int64) | (nb << 16)], -1)
+        self.hdr.copy_(torch.as_tensor(hdr.astype(np.int64).astype(np.uint32).view(np.int32)).to(dev))
+
+    def state_of(self, i, host=None):
+        """Reference-shaped State of env i (numpy, reference dtypes: float32
+        arrays for a fresh game, float64 after its first step)."""
+        h = host or self.to_host()
+        tick = int(h['tick'][i])
+        npl = int(h['nplanets'][i])
+        nb = int(h['nbullets'][i])
+        fresh = tick == 0
+        f = np.float32 if fresh else np.float64
+        ships = h['ships'][i].astype(np.float64)
+        pl = h['planets'][i, :npl].astype(np.float64)
+        bl = h['bullets'][i, :nb].astype(np.float64)
+        pf = np.float32 if (fresh or npl == 1) else np.float64
+        pdxf = np.float32 if npl == 1 else np.float64
+        sch = self.schedule
+        k = min(tick, sch.timeout_tick)
+        return State(
+            ships=Bodies(x=ships[:, 0:2].astype(f), dx=ships[:, 2:4].astype(f),
+                         b=h['ships_b'][i].astype(f)),
+            planets=Bodies(x=pl[:, 0:2].astype(pf), dx=pl[:, 2:4].astype(pdxf), b=None),
+            bullets=Bodies(x=bl[:, 0:2].astype(f), dx=bl[:, 2:4].astype(f), b=None),
+            reload=float(sch.reload[k]), t=float(sch.t[k]))

@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Batched lockstep Astro physics throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3]
+
+One process per GPU (torchrun for N > 1).  Each rank steps its own shard of
+envs (global env ids, no collective on the hot path); a "step" is one
+astro_step launch = one tick of every env on that GPU, auto-reset included.
+Controls are synthetic uniform random actions in [0, 6), keyed by (global
+env id, tick) and resident in HBM before the timed region.  Rank 0 prints
+one JSON line; value = env-steps of ALL ranks / max-over-ranks wall time.
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from astro_amd import BatchedEnv, DEFAULT_CONFIG  # noqa: E402
+from astro_amd import shard as _shard  # noqa: E402
+
+METRIC = 'env-steps/sec (batched lockstep) at 1/2/4/8 MI355X vs CPU core.step'
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# BASELINE.json configs 2, 3 and 5 (per GPU); configs 4 = c3 on 8 GPUs
+WORKLOADS = {
+    'c2': dict(n=4096, cfg=dict(reload_time=1000), b_cap=32, p_pad=4,
+               desc='4096 envs/GPU, DEFAULT_CONFIG with bullets disabled (reload_time=1000), '
+                    '2 ships, 1-4 planets, auto-reset, random actions'),
+    'c3': dict(n=65536, cfg=dict(), b_cap=32, p_pad=4,
+               desc='65536 envs/GPU, DEFAULT_CONFIG (2 ships, 1-4 planets, bullets on, '
+                    'b_cap 32 = 16/ship + overflow counter), auto-reset, random actions'),
+    'c5': dict(n=131072, cfg=dict(max_planets=8), b_cap=32, p_pad=8,
+               desc='131072 envs/GPU, DEFAULT_CONFIG with max_planets=8 (1-8 planets padded '
+                    'to 8), bullets on, auto-reset, random actions'),
+}
+
+
+def controls(offset, n, nships, ticks, seed=0):
+    """int8 [ticks, n, nships] uniform in [0, 6) from splitmix64(global id, tick)."""
+    out = np.empty((ticks, n, nships), dtype=np.int8)
+    ids = (np.arange(offset, offset + n, dtype=np.uint64)[:, None] * np.uint64(nships)
+           + np.arange(nships, dtype=np.uint64)[None, :])
+    with np.errstate(over='ignore'):
+        for t in range(ticks):
+            z = ids * np.uint64(0x9E3779B97F4A7C15) + np.uint64((t + 1) * 0xD1B54A32D192ED03 % (1 << 64)) \
+                + np.uint64(seed)
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(31))
+            out[t] = ((z >> np.uint64(32)) * np.uint64(6) >> np.uint64(32)).astype(np.int8)
+    return out
+
+
+def _cpu_worker(args):
+    cfg_kw, seconds, seed = args
+    from oracle import port
+    return port.run_for(DEFAULT_CONFIG._replace(**cfg_kw), seconds, seed=seed)
+
+
+def cpu_baseline(cfg_kw, seconds, procs):
+    """The single-game numpy port of core.step (oracle/port.py, pinned bit
+    for bit to the reference) on `procs` host cores, one game per process."""
+    if procs == 1:
+        res = [_cpu_worker((cfg_kw, seconds, 0))]
+    else:
+        with mp.get_context('spawn').Pool(procs) as pool:
+            res = pool.map(_cpu_worker, [(cfg_kw, seconds, k) for k in range(procs)])
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return dict(value=steps / wall, unit='env-steps/s', cores=procs, kind='port',
+                sample='%d x %.0f s of single-game oracle/port.py step() (numpy restatement of '
+                       'core.step, bit-exact to the reference), random actions, re-create on '
+                       'termination: %d env-steps' % (procs, seconds, steps),
+                per_core=steps / wall / procs)
+
+
+def algorithmic_bytes(env, dstats, launches):
+    """Bytes a launch must move: per env header r/w (16), ships r/w
+    (2*S*5 elems), control S, reward 4S, done 1; per live planet r/w (8 elems);
+    per live bullet read or written (4 elems); per reset the seed-stream
+    cursor r/w (32)."""
+    e = 8 if env.dtype == torch.float64 else 4
+    S, N = env.S, env.n_env
+    fixed = launches * N * (16 + 2 * S * 5 * e + S + 4 * S + 1)
+    var = (8 * e * dstats['planets'] + 4 * e * (dstats['bullets_in'] + dstats['bullets_out'])
+           + 32 * dstats['resets'])
+    return (fixed + var) / launches
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=1000)
+    ap.add_argument('--warmup', type=int, default=50)
+    ap.add_argument('--workload', default='c3', choices=sorted(WORKLOADS))
+    ap.add_argument('--n-env', type=int, default=0, help='override envs per GPU')
+    ap.add_argument('--state', default='f32', choices=['f32', 'f64'])
+    ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--cpu-procs', type=int, default=1)
+    ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--traffic', default='', help='JSON with PMC-measured HBM bytes per launch')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
+
+    wl = WORKLOADS[args.workload]
+    cfg = DEFAULT_CONFIG._replace(**wl['cfg'])
+    n = args.n_env or wl['n']
+    offset = rank * n
+    env = BatchedEnv(cfg, n, device=dev, b_cap=wl['b_cap'], p_pad=wl['p_pad'],
+                     dtype=torch.float64 if args.state == 'f64' else torch.float32,
+                     env_offset=offset, auto_reset=True)
+    env.reset()
+    ticks = args.warmup + args.steps
+    ctl = torch.from_numpy(controls(offset, n, env.S, ticks)).to(dev)
+    ptrs = [ctl[t].data_ptr() for t in range(ticks)]
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for t in range(args.warmup):
+        env.launch(ptrs[t])
+    barrier()
+    s0 = env.stat_dict()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        a, b = evs[k]
+        a.record(stream)
+        env.launch(ptrs[args.warmup + k])
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    barrier()
+    s1 = env.stat_dict()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    wall_max = _shard.max_over_ranks(wall, device=dev)
+    d = {k: s1[k] - s0[k] for k in s0}
+    tot = _shard.sum_over_ranks([d[k] for k in ('bullets_in', 'resets', 'overflows', 'collisions',
+                                                'timeouts')], device=dev)
+    bytes_launch = algorithmic_bytes(env, d, args.steps)
+
+    if rank == 0:
+        n_total = n * world
+        value = n_total * args.steps / wall_max
+        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if args.traffic and os.path.exists(args.traffic):
+            with open(args.traffic) as f:
+                traffic = json.load(f).get('hbm_bytes_per_launch')
+        out = dict(
+            metric=METRIC, value=value, unit='env-steps/s', n_gpus=world, steps=args.steps,
+            warmup=args.warmup, ms_per_step=wall_max / args.steps * 1e3, higher_is_better=True,
+            scaling='weak', vs_baseline=None,
+            dtype='f64' if args.state == 'f64' else 'f64 math / f32 state',
+            data='synthetic (random actions; games from generate_configs seed streams)',
+            config=dict(workload='%s: %s' % (args.workload, wl['desc']), n_env_per_gpu=n,
+                        n_env_total=n_total, b_cap=wl['b_cap'], p_pad=wl['p_pad'],
+                        state=args.state, parallelism='env-shard x%d (no collectives)' % world),
+            roofline=dict(bound='hbm', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
+                          frac=achieved / HBM_PEAK_GBS, traffic=traffic,
+                          bytes_per_launch=bytes_launch, kernel_ms=kern_ms,
+                          kernel='astro_step_kernel', timing='hipEvent pair per launch'),
+            stats=dict(mean_live_bullets=tot[0] / (n_total * args.steps),
+                       resets_per_step=tot[1] / args.steps, overflow_bullets=tot[2],
+                       collisions=tot[3], timeouts=tot[4],
+                       mean_planets=d['planets'] / (n * args.steps)),
+        )
+        if world == 1 and not args.no_cpu:
+            out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, args.cpu_procs)
+            out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,120 @@
+/*
+ * astro_step.h -- C-ABI of libastro_hip.so, the MI355X (gfx950) batched
+ * lockstep implementation of Astro's per-tick physics.
+ *
+ * The reference (DouglasOrr/Astro) has no FFI: its hot path is the Python
+ * function API of astro/core.py.  Each entry point below replaces one
+ * reference interface, batched over n_env independent games:
+ *
+ *   astro_step         <- core.step(state, control, config)  core.py:215-303
+ *                         (plus auto-reset = core.create(next config of the
+ *                         env's generate_configs stream), core.py:77-135)
+ *   astro_reset        <- core.create(config)                 core.py:86-135
+ *   astro_stream_init  <- core.generate_configs(config)       core.py:77-83
+ *
+ * Conventions
+ *   - The caller owns and allocates all device memory (e.g. PyTorch
+ *     tensors); the library never allocates, frees or synchronises.
+ *   - Every call is stream-ordered and asynchronous on `stream` (a
+ *     hipStream_t passed as void*, NULL = the null stream).
+ *   - Return 0 on success, a negative code on a bad argument (-1..-99) or a
+ *     launch failure (-1000 - hipError_t).  astro_last_error() describes the
+ *     last failure of the calling thread.
+ *   - State is struct-of-arrays, entity-major: slot s of env i lives at
+ *     [s * n_env + i], so consecutive lanes (envs) touch consecutive bytes.
+ *     Element type is float (state_f64 = 0) or double (state_f64 = 1).
+ */
+#ifndef ASTRO_STEP_H
+#define ASTRO_STEP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ASTRO_ABI_VERSION 1
+
+/* Physics constants: the reference Config (core.py:20-41) reduced by the
+ * host exactly as the reference evaluates it, plus the fire/timeout
+ * schedule of its float64 t/reload bookkeeping (core.py:257-302). */
+typedef struct AstroParams {
+    double gm;             /* gravity * planet_mass                 core.py:151 */
+    double dt;             /* dt                                    core.py:189 */
+    double db;             /* dt * ship_rspeed                      core.py:239 */
+    double thrust;         /* ship_thrust                           core.py:234 */
+    double r2_ss;          /* (ship_radius + ship_radius)^2         core.py:211 */
+    double r2_sp;          /* (ship_radius + planet_radius)^2 */
+    double r2_s0;          /* ship_radius^2   (ship <-> bullet) */
+    double r2_p0;          /* planet_radius^2 (planet <-> bullet) */
+    double gravity;        /* create(): planet orbital speed        core.py:121 */
+    double planet_mass;
+    float spawn_off;       /* float32(1.001 * ship_radius)          core.py:273 */
+    float bullet_speed;    /* float32(bullet_speed)                 core.py:277 */
+    float timeout_reward;  /* 1 if solo else 0                      core.py:260 */
+    float outer_pos;       /* float32(outer_ship_position)          core.py:93 */
+    float inner_pos;       /* float32(inner_ship_position)          core.py:95 */
+    float planet_orbit;    /* float32(planet_orbit)                 core.py:119 */
+    int32_t nships;        /* 1 (solo) or 2 */
+    int32_t solo;
+    int32_t max_planets;   /* create(): 1..max_planets planets */
+    int32_t p_pad;         /* planet slots per env, 1..16 (>= max_planets) */
+    int32_t b_cap;         /* bullet slots per env, 1..65535 */
+    int32_t timeout_tick;  /* first tick k with max_time <= t_k + dt */
+    const uint32_t *fire_bits; /* device: bit k = fire on tick k, k < timeout_tick */
+} AstroParams;
+
+/* Per-env state arrays (device pointers).  hdr packs
+ *   hdr[2*i+0] = tick (steps since create)
+ *   hdr[2*i+1] = nplanets | flags << 8 | nbullets << 16
+ * flags: bit0 = a bullet was dropped (b_cap full) this game,
+ *        bit1 = the env's seed stream ran past its 227 exact games. */
+typedef struct AstroState {
+    void *ships;        /* [nships][n_env][4]  x, y, dx, dy */
+    void *ships_b;      /* [nships][n_env]     bearing */
+    void *planets;      /* [p_pad][n_env][4]   x, y, dx, dy */
+    void *bullets;      /* [b_cap][n_env][4]   x, y, dx, dy */
+    int32_t *hdr;       /* [n_env][2] */
+    uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, game seed */
+    int32_t n_env;
+    int32_t state_f64;  /* 0: float arrays, 1: double arrays */
+} AstroState;
+
+/* Statistics accumulated by astro_step when `stats` is non-NULL
+ * (uint64 device counters, added to, never cleared by the library). */
+enum {
+    ASTRO_STAT_BULLETS_IN = 0,  /* live bullets read */
+    ASTRO_STAT_BULLETS_OUT = 1, /* live bullets written */
+    ASTRO_STAT_RESETS = 2,      /* envs re-created by auto-reset */
+    ASTRO_STAT_COLLISIONS = 3,  /* games ended by a ship collision */
+    ASTRO_STAT_TIMEOUTS = 4,    /* games ended by max_time */
+    ASTRO_STAT_OVERFLOWS = 5,   /* bullets dropped for lack of b_cap */
+    ASTRO_STAT_PLANETS = 6,     /* planet slots read */
+    ASTRO_NSTATS = 8
+};
+
+int astro_abi_version(void);
+const char *astro_last_error(void);
+
+/* One tick for every env (core.step).  control: int8 [n_env][nships];
+ * reward: float [n_env][nships]; done: uint8 [n_env] (0 running, 1 ship
+ * collision, 2 timeout).  Running envs advance in place.  A finished env is
+ * re-created from the next seed of its stream when auto_reset != 0 (its
+ * state is otherwise undefined until astro_reset). */
+int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
+               float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset,
+               void *stream);
+
+/* core.create for the envs with mask[i] != 0 (mask NULL = all): from
+ * seeds[i] when seeds != NULL, else from the next seed of env i's stream. */
+int astro_reset(const AstroParams *p, const AstroState *s, const uint32_t *seeds,
+                const uint8_t *mask, void *stream);
+
+/* Position env i's seed stream at generate_configs(seed=stream_seeds[i]). */
+int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ASTRO_STEP_H */

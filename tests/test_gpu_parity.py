@@ -1,0 +1,257 @@
+"""HIP kernel parity: libastro_hip.so (via BatchedEnv) vs the reference's
+golden outputs and vs the CPU oracle.  Needs an MI355X.
+
+Bars
+  * float64 state: bit-exact to the reference (create, teacher-forced steps,
+    whole free-running games).
+  * float32 state: every stored value == float32(reference value computed
+    from the same float32 input state); integer flags/counts/done exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import batched
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+
+CFG = gio.configs()
+
+
+def _env(cfg, n, dtype=torch.float64, b_cap=64, p_pad=8, auto_reset=False):
+    from astro_amd import BatchedEnv
+    return BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, dtype=dtype,
+                      auto_reset=auto_reset)
+
+
+def _host_batch(env):
+    h = env.to_host()
+    return batched.Batch(h['tick'].astype(np.int32), h['nplanets'].astype(np.int32),
+                         h['nbullets'].astype(np.int32), h['ships'].astype(np.float64),
+                         h['ships_b'].astype(np.float64), h['planets'].astype(np.float64),
+                         h['bullets'].astype(np.float64), (h['flags'] & 1).astype(bool))
+
+
+def _assert_same(tag, got, want, run, rounding):
+    """got: Batch from the GPU; want: oracle/reference Batch (float64 values)."""
+    r = (lambda a: a.astype(np.float32).astype(np.float64)) if rounding else (lambda a: a)
+    assert (got.nbullets[run] == want.nbullets[run]).all(), tag
+    assert (got.tick[run] == want.tick[run]).all(), tag
+    assert np.array_equal(got.ships[run], r(want.ships[run])), tag
+    assert np.array_equal(got.ships_b[run], r(want.ships_b[run])), tag
+    pv = (np.arange(got.planets.shape[1])[None, :] < got.nplanets[:, None]) & run[:, None]
+    assert np.array_equal(got.planets[pv], r(want.planets[pv])), tag
+    bv = (np.arange(got.bullets.shape[1])[None, :] < got.nbullets[:, None]) & run[:, None]
+    assert np.array_equal(got.bullets[bv], r(want.bullets[bv])), tag
+
+
+# ------------------------------------------------------------------- create
+
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+@pytest.mark.parametrize('name', sorted(CFG))
+def test_create_matches_reference(name, dtype):
+    z = gio.load('create.npz')
+    cfg = CFG[name]
+    seeds = z[name + '__seed']
+    env = _env(cfg, seeds.size, dtype=dtype, b_cap=4)
+    env.reset(seeds=seeds)
+    h = env.to_host()
+    S = env.S
+    npl = z[name + '__nplanets']
+    assert (h['nplanets'] == npl).all() and (h['tick'] == 0).all() and (h['nbullets'] == 0).all()
+    assert np.array_equal(h['ships'][..., 0:2].astype(np.float32), z[name + '__ships_x'][:, :S])
+    assert not h['ships'][..., 2:4].any()
+    assert np.array_equal(h['ships_b'].astype(np.float32), z[name + '__ships_b'][:, :S])
+    pv = np.arange(8)[None, :] < npl[:, None]
+    assert np.array_equal(h['planets'][..., 0:2][pv].astype(np.float32), z[name + '__planets_x'][pv])
+    want_dx = z[name + '__planets_dx'][pv]
+    if dtype == torch.float32:
+        want_dx = want_dx.astype(np.float32)
+    assert np.array_equal(h['planets'][..., 2:4][pv], want_dx)
+    assert (env.game_seed.cpu().numpy().view(np.uint32) == seeds).all()
+
+
+def test_seed_streams_follow_generate_configs():
+    """Env i's k-th game seed == k-th config of
+    generate_configs(config._replace(seed=stream_seed_i)) (core.py:77-83)."""
+    cfg = CFG['default']
+    env = _env(cfg, 300, dtype=torch.float32)
+    ss = batched.stream_seeds(cfg.seed, 300)
+    assert (env.stream_seeds == ss).all()
+    want = batched.game_seeds(ss, 5)
+    for k in range(5):
+        env.reset()
+        assert (env.game_seed.cpu().numpy().view(np.uint32) == want[:, k]).all()
+
+
+# ------------------------------------------------- teacher-forced transitions
+
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+@pytest.mark.parametrize('fname', ['steps.npz', 'edge_steps.npz'])
+def test_step_teacher_forced_vs_reference(fname, dtype):
+    tr = gio.Transitions(fname)
+    for name, idx in tr.groups():
+        cfg = CFG[name]
+        S = 1 if cfg.solo else 2
+        bcap = tr.max_bullets(idx) + 2
+        B = tr.batch_in(idx, S, b_cap=bcap)
+        env = _env(cfg, idx.size, dtype=dtype, b_cap=bcap)
+        env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
+        ctl = tr.z['control'][idx, :S].astype(np.int8)
+        _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+        E, erew, edone = tr.expected(idx, S, b_cap=bcap)
+        done = done.cpu().numpy()
+        assert (done == edone).all(), name
+        assert np.array_equal(rew.cpu().numpy(), erew.astype(np.float32)), name
+        _assert_same('%s/%s' % (fname, name), _host_batch(env), E, done == 0,
+                     rounding=dtype == torch.float32)
+
+
+# ------------------------------------------------------- free-running games
+
+def test_whole_games_float64_bit_exact():
+    """Every golden game replayed from create(seed) with its open-loop
+    controls: every tick's ship state, bullet count, the game length and the
+    outcome match the reference bit for bit."""
+    games = gio.games()
+    by_cfg = {}
+    for g in games:
+        by_cfg.setdefault(g['cfg'], []).append(g)
+    for name, gs in by_cfg.items():
+        cfg = CFG[name]
+        S = 1 if cfg.solo else 2
+        env = _env(cfg, len(gs), dtype=torch.float64, b_cap=512)
+        env.reset(seeds=np.array([g['seed'] for g in gs], dtype=np.uint32))
+        T = max(g['ships'].shape[0] for g in gs)
+        alive = np.ones(len(gs), bool)
+        for t in range(T):
+            h = env.to_host()
+            for k, g in enumerate(gs):
+                if alive[k]:
+                    assert np.array_equal(h['ships'][k], g['ships'][t, :S, 0:4]), (name, g['gid'], t)
+                    assert np.array_equal(h['ships_b'][k], g['ships'][t, :S, 4]), (name, g['gid'], t)
+                    assert h['nbullets'][k] == g['nbullets'][t], (name, g['gid'], t)
+            ctl = np.full((len(gs), S), 2, np.int8)
+            for k, g in enumerate(gs):
+                if alive[k]:
+                    ctl[k] = g['controls'][t]
+            _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+            done = done.cpu().numpy()
+            rew = rew.cpu().numpy()
+            for k, g in enumerate(gs):
+                if not alive[k]:
+                    continue
+                last = t == g['ships'].shape[0] - 1
+                assert bool(done[k]) == last, (name, g['gid'], t)
+                if last:
+                    assert done[k] == g['done'] and np.array_equal(rew[k], g['reward'][:S])
+                    alive[k] = False
+        assert not alive.any()
+
+
+# ----------------------------------------- batched run vs oracle, auto-reset
+
+@pytest.mark.parametrize('name,n,ticks,bcap', [('default', 4096, 60, 32), ('mp8', 2000, 40, 32),
+                                              ('rapid', 512, 30, 6), ('solo', 700, 40, 32)])
+def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap):
+    """N envs with auto-reset, float32 state: every tick equals the oracle
+    stepped from the kernel's own input state, resets draw the right seeds
+    and create the right games, overflow (small b_cap) is counted alike."""
+    cfg = CFG[name]
+    P = batched.make_params(cfg)
+    env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, auto_reset=True)
+    env.reset()
+    seeds = batched.game_seeds(env.stream_seeds, 64)
+    games = np.ones(n, np.int64)          # game 0 was created by reset()
+    rng = np.random.RandomState(1)
+    for t in range(ticks):
+        B = _host_batch(env)
+        ctl = rng.randint(0, 6, size=(n, env.S)).astype(np.int8)
+        want, wrew, wdone = batched.step(B, ctl, P, store='f32')
+        fin = np.nonzero(wdone)[0]
+        if fin.size:
+            fresh = batched.create(seeds[fin, games[fin]], P, p_pad=env.p_pad, b_cap=bcap, store='f32')
+            want.put(fin, fresh)
+            games[fin] += 1
+        _, rew, done = env.step(torch.from_numpy(ctl).cuda())
+        done = done.cpu().numpy()
+        assert (done == wdone).all(), t
+        assert np.array_equal(rew.cpu().numpy(), wrew), t
+        got = _host_batch(env)
+        _assert_same('%s t=%d' % (name, t), got, want, np.ones(n, bool), rounding=True)
+        assert (got.overflow == want.overflow).all(), t
+    st = env.stat_dict()
+    assert st['resets'] == int((games - 1).sum())
+    if name == 'rapid':
+        assert st['overflows'] > 0
+
+
+# ------------------------------------------------------- shapes / edge cases
+
+@pytest.mark.parametrize('n', [1, 63, 65, 1000])
+def test_ragged_env_counts(n):
+    cfg = CFG['default']
+    env = _env(cfg, n, dtype=torch.float32, b_cap=32, auto_reset=True)
+    env.reset()
+    P = batched.make_params(cfg)
+    B = _host_batch(env)
+    ctl = np.random.RandomState(n).randint(0, 6, size=(n, 2)).astype(np.int8)
+    want, wrew, wdone = batched.step(B, ctl, P, store='f32')
+    _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+    assert (done.cpu().numpy() == wdone).all()
+    _assert_same('n=%d' % n, _host_batch(env), want, wdone == 0, rounding=True)
+
+
+def test_zero_envs_is_a_noop():
+    cfg = CFG['default']
+    env = _env(cfg, 0, dtype=torch.float32)
+    env.reset()
+    env.step(torch.zeros((0, 2), dtype=torch.int8, device='cuda'))
+    torch.cuda.synchronize()
+
+
+def test_bad_arguments_raise():
+    from astro_amd import _lib
+    cfg = CFG['default']
+    env = _env(cfg, 8, dtype=torch.float32)
+    with pytest.raises(ValueError):
+        env.step(torch.zeros((8, 3), dtype=torch.int8, device='cuda'))
+    bad = type(env.params).from_buffer_copy(env.params)
+    bad.nships = 3
+    env.params, good = bad, env.params
+    with pytest.raises(_lib.AstroError):
+        env.step(torch.zeros((8, 2), dtype=torch.int8, device='cuda'))
+    env.params = good
+
+
+# ------------------------------------------------ size-independent properties
+
+def test_full_size_determinism_and_shard_invariance():
+    """65,536 envs (BASELINE config 3): two identical runs agree bit for bit,
+    and two half-size shards with global env ids reproduce the full run."""
+    cfg = CFG['default']
+    n, ticks = 65536, 200
+    g = torch.Generator(device='cuda').manual_seed(0)
+    ctls = torch.randint(0, 6, (ticks, n, 2), generator=g, device='cuda', dtype=torch.int8)
+
+    def run(offset, count):
+        from astro_amd import BatchedEnv
+        env = BatchedEnv(cfg, count, device='cuda:0', b_cap=32, env_offset=offset)
+        env.reset()
+        for t in range(ticks):
+            env.step(ctls[t, offset:offset + count].contiguous())
+        return env
+    a = run(0, n)
+    b = run(0, n)
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    lo = run(0, n // 2)
+    hi = run(n // 2, n // 2)
+    assert torch.equal(torch.cat([lo.hdr, hi.hdr]), a.hdr)
+    assert torch.equal(torch.cat([lo.stream, hi.stream]), a.stream)
+    assert torch.equal(torch.cat([lo.ships, hi.ships], 1), a.ships)
+    nb = a.nbullets
+    assert int(nb.max()) <= 32 and int(a.nplanets.min()) >= 1 and int(a.nplanets.max()) <= 4
+    st = a.stat_dict()
+    assert st['resets'] == st['collisions'] + st['timeouts'] > 0

@@ -1,0 +1,145 @@
+"""CPU-only checks of the boundary and the host logic (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import __graft_entry__
+from astro_amd import _lib, schedule, shard
+from astro_amd.config import DEFAULT_CONFIG, SOLO_CONFIG, generate_configs
+from oracle import batched
+from tests import golden_io as gio
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'astro_step.h')
+
+
+@pytest.fixture(scope='module')
+def lib():
+    __graft_entry__.build()
+    return _lib.load()
+
+
+def _declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r'^\s*(?:const\s+)?\w+\s*\*?\s*(astro_\w+)\s*\(', text, re.M)))
+
+
+def test_library_exports_every_header_symbol(lib):
+    names = _declared_functions()
+    assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_reset',
+                          'astro_stream_init'}
+    out = subprocess.check_output(['nm', '-D', '--defined-only', _lib.LIB_PATH], text=True)
+    exported = set(re.findall(r' T (astro_\w+)$', out, re.M))
+    assert set(names) <= exported
+    for n in names:
+        getattr(lib, n)
+    assert lib.astro_abi_version() == _lib.ABI_VERSION
+
+
+def test_ctypes_struct_layout_matches_header():
+    """sizeof/offsetof of the C structs (gcc on include/astro_step.h) equal
+    the ctypes mirrors'."""
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "astro_step.h"', 'int main(void){']
+    expect = []
+    for st in (_lib.AstroParams, _lib.AstroState):
+        lines.append('printf("%%zu\\n", sizeof(%s));' % st.__name__)
+        expect.append(ctypes.sizeof(st))
+        for f, _ in st._fields_:
+            lines.append('printf("%%zu\\n", offsetof(%s, %s));' % (st.__name__, f))
+            expect.append(getattr(st, f).offset)
+    lines.append('return 0;}')
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, 'layout.c')
+        exe = os.path.join(d, 'layout')
+        open(src, 'w').write('\n'.join(lines))
+        subprocess.check_call(['gcc', '-std=c99', '-I', os.path.dirname(HEADER), src, '-o', exe])
+        got = [int(x) for x in subprocess.check_output([exe], text=True).split()]
+    assert got == expect
+
+
+def test_argument_validation_without_gpu(lib):
+    """Bad arguments are rejected before any HIP call, with a message."""
+    p = _lib.AstroParams(nships=3, solo=0, p_pad=4, max_planets=4, b_cap=32)
+    s = _lib.AstroState(n_env=4)
+    rc = lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None)
+    assert rc == -11 and b'nships' in lib.astro_last_error()
+    p.nships = 2
+    p.p_pad = 17
+    rc = lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None)
+    assert rc == -13
+    p.p_pad = 4
+    s.n_env = -1
+    assert lib.astro_reset(ctypes.byref(p), ctypes.byref(s), None, None, None) == -3
+    s.n_env = 0   # empty batch: a no-op that never touches the device
+    assert lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None) == 0
+    assert lib.astro_stream_init(ctypes.byref(s), None, None) == 0
+    assert lib.astro_step(None, ctypes.byref(s), None, None, None, None, 0, None) == -10
+
+
+def test_schedule_matches_oracle_and_golden():
+    sched = gio.load_json('schedule.json')
+    for name, s in sched.items():
+        cfg = DEFAULT_CONFIG._replace(**s['config'])
+        sc = schedule.build(cfg)
+        assert sc.timeout_tick == s['timeout_tick']
+        bits = sc.fire_bits()
+        fired = [k for k in range(sc.timeout_tick) if (bits[k >> 5] >> (k & 31)) & 1]
+        assert fired == s['fire_ticks'], name
+        assert sc.t[:50].tolist() == s['t'] and sc.reload[:50].tolist() == s['reload']
+
+
+def test_kernel_constants_match_oracle():
+    for cfg in gio.configs().values():
+        k = schedule.kernel_constants(cfg)
+        P = batched.make_params(cfg)
+        for f in ('gm', 'db', 'r2_ss', 'r2_sp', 'r2_s0', 'r2_p0'):
+            assert k[f] == getattr(P, f), f
+        assert np.float32(k['spawn_off']) == P.spawn_off
+        assert np.float32(k['bullet_speed']) == P.bullet_speed
+        assert k['nships'] == P.nships
+
+
+def test_generate_configs_matches_golden():
+    z = gio.load('generate_configs.npz')
+    import itertools as it
+    for key in z.files:
+        seed = int(key.split('_', 1)[1])
+        got = [c.seed for c in it.islice(generate_configs(DEFAULT_CONFIG._replace(seed=seed)), 300)]
+        assert got == z[key].tolist()
+
+
+def test_presets_match_reference_values():
+    cfgs = gio.configs()
+    assert cfgs['default'] == DEFAULT_CONFIG
+    assert cfgs['solo'] == SOLO_CONFIG
+
+
+@pytest.mark.parametrize('n,world', [(524288, 8), (1048576, 8), (65536, 1), (1001, 4), (3, 8)])
+def test_shard_ranges_partition(n, world):
+    seen = []
+    for r in range(world):
+        off, cnt = shard.shard(n, r, world)
+        seen.extend(range(off, off + cnt))
+    assert seen == list(range(n))
+
+
+def test_wrap_formula_matches_numpy_remainder():
+    """The kernel's wrap (fmod, +2 if negative, +0 if zero, -1) equals numpy's
+    ((x + 1) % 2) - 1 (util.py:148) on random and edge values."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(-3, 3, 100000), rng.uniform(-1e-15, 1e-15, 1000),
+                        [-1.0, 1.0, 3.0, -3.0, 0.0, -0.0, 1 - 2 ** -53, -1 + 2 ** -53, 2.0 ** -1074]])
+    m = np.fmod(x + 1.0, 2.0)
+    m = np.where(m != 0, np.where(m < 0, m + 2.0, m), 0.0)
+    mine = m - 1.0
+    ref = ((x + 1) % 2) - 1
+    assert (mine.view(np.int64) == ref.view(np.int64)).all()
+    x32 = x.astype(np.float32)
+    m = np.fmod(x32 + np.float32(1), np.float32(2))
+    m = np.where(m != 0, np.where(m < 0, m + np.float32(2), m), np.float32(0)).astype(np.float32)
+    assert ((m - np.float32(1)).view(np.int32) == (((x32 + 1) % 2) - 1).view(np.int32)).all()

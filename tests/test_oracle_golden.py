@@ -157,3 +157,64 @@ def test_games_free_running_float64_bit_exact():
                 assert done[0] == 0
         assert done[0] == g['done'], g['gid']
         assert np.array_equal(rew[0], g['reward'][:S].astype(np.float32))
+
+
+# ------------------------------------------------------- single-game port
+
+def _state_from_row(tr, i, S):
+    from oracle import port
+    z = tr.z
+    fl = int(z['dtype_flags'][i])
+    sf = np.float32 if fl & 1 else np.float64
+    pxf = np.float32 if fl & 2 else np.float64
+    pdf = np.float32 if fl & 4 else np.float64
+    bf = np.float32 if fl & 8 else np.float64
+    sh = z['in_ships'][i, :S]
+    n = z['nplanets'][i]
+    pl = z['in_planets'][i, :n]
+    off = z['in_bullets_off']
+    bl = z['in_bullets'][off[i]:off[i + 1]]
+    return port.State(ships=port.Bodies(sh[:, 0:2].astype(sf), sh[:, 2:4].astype(sf), sh[:, 4].astype(sf)),
+                      planets=port.Bodies(pl[:, 0:2].astype(pxf), pl[:, 2:4].astype(pdf), None),
+                      bullets=port.Bodies(bl[:, 0:2].astype(bf), bl[:, 2:4].astype(bf), None),
+                      reload=0.0, t=0.0)
+
+
+def test_port_step_teacher_forced_bit_exact():
+    """The single-game CPU port (timed CPU baseline) == reference, on every
+    golden transition; reload/t come from the schedule of the tick."""
+    from oracle import port
+    tr = gio.Transitions('steps.npz')
+    for name, idx in tr.groups():
+        cfg = CFG[name]
+        g = port.Game(cfg)
+        S = g.ns
+        _, _, ts, reloads = batched.schedule(cfg)
+        for i in idx[::3]:
+            st = _state_from_row(tr, i, S)
+            k = int(tr.z['tick'][i])
+            st = st._replace(t=float(ts[k]), reload=float(reloads[k]))
+            out, rew = g.step(st, tr.z['control'][i, :S].astype(np.int64))
+            done = tr.z['out_done'][i]
+            assert (out is None) == (done != 0)
+            assert np.array_equal(rew, tr.z['out_reward'][i, :S])
+            if out is None:
+                continue
+            assert np.array_equal(out.ships.x, tr.z['out_ships'][i, :S, 0:2])
+            assert np.array_equal(out.ships.b, tr.z['out_ships'][i, :S, 4])
+            n = tr.z['nplanets'][i]
+            assert np.array_equal(out.planets.dx, tr.z['out_planets'][i, :n, 2:4])
+            off = tr.z['out_bullets_off']
+            assert np.array_equal(out.bullets.x, tr.z['out_bullets'][off[i]:off[i + 1], 0:2])
+
+
+def test_port_create_bit_exact():
+    from oracle import port
+    z = gio.load('create.npz')
+    for name in ('default', 'mp8', 'solo'):
+        g = port.Game(CFG[name])
+        for k, seed in enumerate(z[name + '__seed'][:64]):
+            s = g.create(int(seed))
+            n = s.planets.x.shape[0]
+            assert np.array_equal(s.ships.x, z[name + '__ships_x'][k, :g.ns])
+            assert np.array_equal(s.planets.dx, z[name + '__planets_dx'][k, :n])
