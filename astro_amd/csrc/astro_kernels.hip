@@ -88,15 +88,16 @@ __device__ __forceinline__ void np_sincosf(float x, float &s_out, float &c_out) 
 }
 
 // util.wrap_unit_square (util.py:145-148): ((v + 1) % 2) - 1 with numpy's
-// floored remainder (npy_divmod: fmod, then +2 when negative, +0 when zero).
+// floored remainder (npy_divmod: fmod, then +2 when negative, +0 when
+// zero).  fmod(x, 2) == x - 2*trunc(x/2) EXACTLY for finite x: x/2 and
+// 2*trunc are exact, and x - 2t is exact by Sterbenz (2t and x share sign,
+// |2t| <= |x| < |2t| + 2).  Five instructions instead of ocml's fmod loop.
 template <typename C>
 __device__ __forceinline__ C wrap_unit(C v) {
-    C m = fmod(v + C(1), C(2));
-    if (m != C(0)) {
-        if (m < C(0)) m = m + C(2);
-    } else {
-        m = C(0);
-    }
+    const C x = v + C(1);
+    C m = x - C(2) * trunc(x * C(0.5));
+    m = m < C(0) ? m + C(2) : m;
+    m = m == C(0) ? C(0) : m;
     return m - C(1);
 }
 
@@ -141,6 +142,65 @@ __device__ __forceinline__ double dist2(double ax, double ay, double bx, double 
     const C dx = C(ax) - C(bx);
     const C dy = C(ay) - C(by);
     return double(dx * dx + dy * dy);
+}
+
+// Planet-on-planet gravity (core.py:291) for every planet i < np, in the
+// reference's summation order (j = 0..np-1, self term +0.0 included).  The
+// pair (i, j) and (j, i) share d2 bit for bit and their terms are exact
+// negatives, so each gm / max(1e-12, d2) is computed once: np(np-1)/2
+// divisions instead of np^2.
+template <typename C, int PMAX>
+__device__ __forceinline__ void planet_field(const double (&px)[PMAX], const double (&py)[PMAX], int np,
+                                             double gm, C (&gx)[PMAX], C (&gy)[PMAX]) {
+    if constexpr (PMAX > 8) {
+        // a 16x16 table of pair factors would not fit in registers: direct form
+#pragma unroll
+        for (int i = 0; i < PMAX; ++i) {
+            if (i < np) field<C, PMAX>(px, py, np, px[i], py[i], gm, gx[i], gy[i]);
+        }
+        return;
+    }
+    C f[PMAX][PMAX];
+#pragma unroll
+    for (int i = 0; i < PMAX; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < PMAX; ++j) {
+            if (j < np) {
+                const C rx = C(px[j]) - C(px[i]);
+                const C ry = C(py[j]) - C(py[i]);
+                f[i][j] = C(gm) / max_floor(rx * rx + ry * ry);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PMAX; ++i) {
+        C ax = C(0), ay = C(0);
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+            if (j < np) {
+                C tx, ty;
+                if (j == i) {
+                    tx = C(0);
+                    ty = C(0);
+                } else {
+                    const C rx = C(px[j]) - C(px[i]);
+                    const C ry = C(py[j]) - C(py[i]);
+                    const C fij = j > i ? f[i][j] : f[j][i];
+                    tx = fij * rx;
+                    ty = fij * ry;
+                }
+                if (j == 0) {
+                    ax = tx;
+                    ay = ty;
+                } else {
+                    ax = ax + tx;
+                    ay = ay + ty;
+                }
+            }
+        }
+        gx[i] = ax;
+        gy[i] = ay;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -311,7 +371,7 @@ __device__ __forceinline__ uint32_t stream_next(const AstroState &st, int i, boo
     return seed;
 }
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
@@ -322,6 +382,91 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 
 constexpr int BLOCK = 64;
 constexpr int BCHUNK = 8;  // bullets loaded per batch: 8 loads in flight per lane
+
+// One bullet pass in precision C (float at tick 0, double after): collide
+// every live bullet with the OLD planets and ships (core.py:241-251), drop the
+// hit ones (core.py:264-266), move the rest without gravity and cull those
+// with BOTH coordinates outside [-1, 1] (core.py:295-300, 195), compacting in
+// order, in place (slot written <= slot read).
+template <typename C, typename T, int S, int PMAX>
+__device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store<T>::V *bullets, size_t NN, int i,
+                                            int nb, int np, const double (&px)[PMAX], const double (&py)[PMAX],
+                                            const double (&sx)[S], const double (&sy)[S],
+                                            typename Store<T>::V (&buf)[BCHUNK], bool (&hit)[S], int &w,
+                                            int &dropped) {
+    using V = typename Store<T>::V;
+    const C dt = C(p.dt);
+    for (int base = 0; base < nb; base += BCHUNK) {
+        if (base > 0) {
+#pragma unroll
+            for (int u = 0; u < BCHUNK; ++u) {
+                const int k = base + u < nb ? base + u : 0;
+                buf[u] = bullets[size_t(k) * NN + i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < BCHUNK; ++u) {
+            if (base + u < nb) {
+                const double x = double(buf[u].x), y = double(buf[u].y);
+                bool bh = false;
+#pragma unroll
+                for (int j = 0; j < PMAX; ++j)
+                    if (j < np) bh = bh || dist2<C>(x, y, px[j], py[j]) < p.r2_p0;
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const bool hs = dist2<C>(x, y, sx[s], sy[s]) < p.r2_s0;
+                    bh = bh || hs;
+                    hit[s] = hit[s] || hs;
+                }
+                if (!bh) {
+                    const C ndx = C(buf[u].z) + C(0), ndy = C(buf[u].w) + C(0);
+                    const C nx = C(x) + dt * ndx, ny = C(y) + dt * ndy;
+                    const bool keep = (C(-1) <= nx && nx <= C(1)) || (C(-1) <= ny && ny <= C(1));
+                    const bool fits = w < p.b_cap;
+                    if (keep && fits) {
+                        V v;
+                        v.x = T(nx);
+                        v.y = T(ny);
+                        v.z = T(ndx);
+                        v.w = T(ndy);
+                        bullets[size_t(w) * NN + i] = v;
+                    }
+                    // counters as arithmetic: a conditional ++ of one of two
+                    // locals is folded into a store through a selected
+                    // pointer, which sends both to scratch memory
+                    w += int(keep && fits);
+                    dropped += int(keep && !fits);
+                }
+            }
+        }
+    }
+}
+
+// New bullet of one ship (core.py:267-279) moved and culled like the others.
+template <typename C, typename T>
+__device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V *bullets, size_t NN, int i,
+                                      double sx, double sy, double sdx, double sdy, float ds, float dc, int &w,
+                                      int &dropped) {
+    using V = typename Store<T>::V;
+    const float os = p.spawn_off * ds, oc = p.spawn_off * dc;
+    const float vs = p.bullet_speed * ds, vc = p.bullet_speed * dc;
+    const C bx = C(sx) + C(os), by = C(sy) + C(oc);
+    const C bdx = (C(sdx) + C(vs)) + C(0), bdy = (C(sdy) + C(vc)) + C(0);
+    const C dt = C(p.dt);
+    const C nx = bx + dt * bdx, ny = by + dt * bdy;
+    const bool keep = (C(-1) <= nx && nx <= C(1)) || (C(-1) <= ny && ny <= C(1));
+    const bool fits = w < p.b_cap;
+    if (keep && fits) {
+        V v;
+        v.x = T(nx);
+        v.y = T(ny);
+        v.z = T(bdx);
+        v.w = T(bdy);
+        bullets[size_t(w) * NN + i] = v;
+    }
+    w += int(keep && fits);
+    dropped += int(keep && !fits);
+}
 
 template <typename T, int S, int PMAX>
 __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroState st,
@@ -334,7 +479,8 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
     const int N = st.n_env;
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool active = i < N;
-    uint64_t st_bin = 0, st_bout = 0, st_reset = 0, st_coll = 0, st_tout = 0, st_ovf = 0, st_pl = 0;
+    uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
+    bool f_reset = false, f_coll = false, f_tout = false;
 
     if (active) {
         const size_t NN = size_t(N);
@@ -343,14 +489,8 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         V *planets = reinterpret_cast<V *>(st.planets);
         V *bullets = reinterpret_cast<V *>(st.bullets);
 
+        // ---- round 1 of loads: header, ships, control (independent)
         const int2 h = reinterpret_cast<const int2 *>(st.hdr)[i];
-        const int tick = h.x;
-        int np = h.y & 0xff;
-        int flags = (h.y >> 8) & 0xff;
-        const int nb = int(uint32_t(h.y) >> 16);
-        np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
-
-        // ---- loads: ships, planets (padded slots re-read slot 0), control
         double sx[S], sy[S], sdx[S], sdy[S], sb[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -361,6 +501,24 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             sdy[s] = double(v.w);
             sb[s] = double(ships_b[size_t(s) * NN + i]);
         }
+        int ctl[S];
+        if (S == 2) {
+            const uint16_t c2 = reinterpret_cast<const uint16_t *>(control)[i];
+            ctl[0] = int(int8_t(c2 & 0xff));
+            ctl[S - 1] = int(int8_t(c2 >> 8));
+        } else {
+            ctl[0] = int(control[i]);
+        }
+        const int tick = h.x;
+        int np = h.y & 0xff;
+        int flags = (h.y >> 8) & 0xff;
+        const int nb = int(uint32_t(h.y) >> 16);
+        np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+        const bool live = tick < p.timeout_tick;
+        const bool t0 = tick == 0;
+
+        // ---- round 2 (needs the header): planets (padded slots re-read
+        //      slot 0), the fire word, the first bullet chunk
         double px[PMAX], py[PMAX], pdx[PMAX], pdy[PMAX];
 #pragma unroll
         for (int j = 0; j < PMAX; ++j) {
@@ -371,20 +529,17 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             pdx[j] = double(v.z);
             pdy[j] = double(v.w);
         }
-        int ctl[S];
-        if (S == 2) {
-            const uint16_t c2 = reinterpret_cast<const uint16_t *>(control)[i];
-            ctl[0] = int(int8_t(c2 & 0xff));
-            ctl[S - 1] = int(int8_t(c2 >> 8));
-        } else {
-            ctl[0] = int(control[i]);
+        const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
+        V buf[BCHUNK];
+#pragma unroll
+        for (int u = 0; u < BCHUNK; ++u) {
+            const int k = u < nb ? u : 0;
+            buf[u] = bullets[size_t(k) * NN + i];
         }
-        st_pl = uint64_t(np);
-
-        const bool t0 = tick == 0;
+        n_pl = uint32_t(np);
 
         // ---- ship acceleration (core.py:234-239): thrust along direction(b)
-        //      + gravity; floor //2 and %2 of the control code
+        //      + gravity; floored //2 and %2 of the control code
         float ds[S], dc[S];
         double ax[S], ay[S], dbear[S];
 #pragma unroll
@@ -429,72 +584,13 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             hit[S - 1] = hit[S - 1] || hh;
         }
 
-        // ---- bullet pass: collide (old positions), then survivors move
-        //      without gravity and are culled when both coords leave [-1, 1]
-        //      (core.py:264-266, 295-300, 195), compacted in order in place
-        const bool live = tick < p.timeout_tick;
-        const bool fire = live && ((p.fire_bits[tick >> 5] >> (tick & 31)) & 1u);
-        int w = 0;         // bullets written
-        int dropped = 0;   // bullets lost to b_cap
-        const int bcap = p.b_cap;
-
-        auto emit = [&](double x, double y, double dx, double dy) {
-            if (w < bcap) {
-                V v;
-                v.x = T(x);
-                v.y = T(y);
-                v.z = T(dx);
-                v.w = T(dy);
-                bullets[size_t(w) * NN + i] = v;
-                ++w;
-            } else {
-                ++dropped;
-            }
-        };
-        // one bullet: returns nothing, updates hit[] and emits the survivor
-        auto bullet = [&](const V &v) {
-            const double x = double(v.x), y = double(v.y), dx = double(v.z), dy = double(v.w);
-            bool bh = false;
-#pragma unroll
-            for (int j = 0; j < PMAX; ++j) {
-                if (j < np) {
-                    const double d2 = t0 ? dist2<float>(x, y, px[j], py[j])
-                                         : dist2<double>(x, y, px[j], py[j]);
-                    bh = bh || d2 < p.r2_p0;
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const double d2 = t0 ? dist2<float>(x, y, sx[s], sy[s]) : dist2<double>(x, y, sx[s], sy[s]);
-                const bool hs = d2 < p.r2_s0;
-                bh = bh || hs;
-                hit[s] = hit[s] || hs;
-            }
-            if (!bh) {
-                if (t0) {
-                    const float ndx = float(dx) + 0.0f, ndy = float(dy) + 0.0f;
-                    const float dtf = float(p.dt);
-                    const float nx = float(x) + dtf * ndx, ny = float(y) + dtf * ndy;
-                    if ((-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f)) emit(nx, ny, ndx, ndy);
-                } else {
-                    const double ndx = dx + 0.0, ndy = dy + 0.0;
-                    const double nx = x + p.dt * ndx, ny = y + p.dt * ndy;
-                    if ((-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0)) emit(nx, ny, ndx, ndy);
-                }
-            }
-        };
-        for (int base = 0; base < nb; base += BCHUNK) {
-            V buf[BCHUNK];
-#pragma unroll
-            for (int u = 0; u < BCHUNK; ++u) {
-                const int k = base + u < nb ? base + u : 0;
-                buf[u] = bullets[size_t(k) * NN + i];
-            }
-#pragma unroll
-            for (int u = 0; u < BCHUNK; ++u)
-                if (base + u < nb) bullet(buf[u]);
-        }
-        st_bin = uint64_t(nb);
+        // ---- bullets
+        int w = 0, dropped = 0;
+        if (t0)
+            bullet_pass<float, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped);
+        else
+            bullet_pass<double, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped);
+        n_bin = uint32_t(nb);
 
         const bool collided = S == 2 ? (hit[0] || hit[S - 1]) : hit[0];
         const bool timeout = !collided && !live;
@@ -513,25 +609,14 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         done_out[i] = done;
 
         if (!done) {
-            // ---- fire: one new bullet per ship from the OLD ship state,
-            //      appended after the survivors (core.py:267-280)
-            if (fire) {
-                const float dtf = float(p.dt);
+            // ---- fire from the OLD ship state, after the survivors (core.py:267-280)
+            if ((fire_word >> (tick & 31)) & 1u) {
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
-                    const float os = p.spawn_off * ds[s], oc = p.spawn_off * dc[s];
-                    const float vs = p.bullet_speed * ds[s], vc = p.bullet_speed * dc[s];
-                    if (t0) {
-                        const float bx = float(sx[s]) + os, by = float(sy[s]) + oc;
-                        const float bdx = float(sdx[s]) + vs + 0.0f, bdy = float(sdy[s]) + vc + 0.0f;
-                        const float nx = bx + dtf * bdx, ny = by + dtf * bdy;
-                        if ((-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f)) emit(nx, ny, bdx, bdy);
-                    } else {
-                        const double bx = sx[s] + double(os), by = sy[s] + double(oc);
-                        const double bdx = (sdx[s] + double(vs)) + 0.0, bdy = (sdy[s] + double(vc)) + 0.0;
-                        const double nx = bx + p.dt * bdx, ny = by + p.dt * bdy;
-                        if ((-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0)) emit(nx, ny, bdx, bdy);
-                    }
+                    if (t0)
+                        spawn<float, T>(p, bullets, NN, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
+                    else
+                        spawn<double, T>(p, bullets, NN, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
                 }
             }
 
@@ -549,73 +634,94 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                 ships_b[size_t(s) * NN + i] = T(sb[s] + dbear[s]);
             }
 
-            // ---- planets: mutual gravity incl. the (zero) self term
-            //      (core.py:289-294); float32 at tick 0 / for a lone planet
+            // ---- planets: mutual gravity (core.py:289-294); float32 at tick 0
+            //      (create's float32 positions) and for a lone planet (its
+            //      arrays stay float32 for the whole game)
             const float dtf = float(p.dt);
+            if (np == 1) {
+                float gx, gy;
+                field<float, PMAX>(px, py, 1, px[0], py[0], p.gm, gx, gy);
+                const float ndx = float(pdx[0]) + gx * dtf;
+                const float ndy = float(pdy[0]) + gy * dtf;
+                V v;
+                v.x = T(wrap_unit<float>(float(px[0]) + dtf * ndx));
+                v.y = T(wrap_unit<float>(float(py[0]) + dtf * ndy));
+                v.z = T(ndx);
+                v.w = T(ndy);
+                planets[i] = v;
+            } else {
+                double gx[PMAX], gy[PMAX];
+                if (t0) {
+                    float fx[PMAX], fy[PMAX];
+                    planet_field<float, PMAX>(px, py, np, p.gm, fx, fy);
 #pragma unroll
-            for (int j = 0; j < PMAX; ++j) {
-                if (j < np) {
-                    V v;
-                    if (np == 1) {
-                        float gx, gy;
-                        field<float, PMAX>(px, py, np, px[j], py[j], p.gm, gx, gy);
-                        const float ndx = float(pdx[j]) + gx * dtf;
-                        const float ndy = float(pdy[j]) + gy * dtf;
-                        v.x = T(wrap_unit<float>(float(px[j]) + dtf * ndx));
-                        v.y = T(wrap_unit<float>(float(py[j]) + dtf * ndy));
-                        v.z = T(ndx);
-                        v.w = T(ndy);
-                    } else {
-                        double ndx, ndy;
-                        if (t0) {
-                            float gx, gy;
-                            field<float, PMAX>(px, py, np, px[j], py[j], p.gm, gx, gy);
-                            ndx = pdx[j] + double(gx * dtf);
-                            ndy = pdy[j] + double(gy * dtf);
-                        } else {
-                            double gx, gy;
-                            field<double, PMAX>(px, py, np, px[j], py[j], p.gm, gx, gy);
-                            ndx = pdx[j] + gx * p.dt;
-                            ndy = pdy[j] + gy * p.dt;
-                        }
+                    for (int j = 0; j < PMAX; ++j) {
+                        gx[j] = double(fx[j] * dtf);   // float32 a * dt, then float64 add
+                        gy[j] = double(fy[j] * dtf);
+                    }
+                } else {
+                    planet_field<double, PMAX>(px, py, np, p.gm, gx, gy);
+#pragma unroll
+                    for (int j = 0; j < PMAX; ++j) {
+                        gx[j] = gx[j] * p.dt;
+                        gy[j] = gy[j] * p.dt;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < PMAX; ++j) {
+                    if (j < np) {
+                        const double ndx = pdx[j] + gx[j];
+                        const double ndy = pdy[j] + gy[j];
+                        V v;
                         v.x = T(wrap_unit<double>(px[j] + p.dt * ndx));
                         v.y = T(wrap_unit<double>(py[j] + p.dt * ndy));
                         v.z = T(ndx);
                         v.w = T(ndy);
+                        planets[size_t(j) * NN + i] = v;
                     }
-                    planets[size_t(j) * NN + i] = v;
                 }
             }
             if (dropped) flags |= 1;
             reinterpret_cast<int2 *>(st.hdr)[i] = make_int2(tick + 1, np | (flags << 8) | (w << 16));
-            st_bout = uint64_t(w);
-            st_ovf = uint64_t(dropped);
+            n_bout = uint32_t(w);
+            n_drop = uint32_t(dropped);
         } else {
-            st_coll = collided ? 1 : 0;
-            st_tout = timeout ? 1 : 0;
+            f_coll = collided;
+            f_tout = timeout;
             if (auto_reset) {
                 bool exhausted;
                 const uint32_t seed = stream_next(st, i, exhausted);
                 int cf = 0;
                 create_env<T, S, PMAX>(p, st, i, seed, cf);
                 if (exhausted || cf) st.hdr[2 * i + 1] |= 2 << 8;
-                st_reset = 1;
+                f_reset = true;
             }
         }
     }
 
+    // ---- statistics: one private slot per wave (contention-free no-return
+    //      atomics; summed over slots by the host)
     if (stats) {
-        const uint64_t a = wave_sum(st_bin), b = wave_sum(st_bout), c = wave_sum(st_reset);
-        const uint64_t d = wave_sum(st_coll), e = wave_sum(st_tout), f = wave_sum(st_ovf);
-        const uint64_t g = wave_sum(st_pl);
+        const uint64_t m_reset = __ballot(f_reset), m_coll = __ballot(f_coll), m_tout = __ballot(f_tout);
+        // per-lane counts are < 2^16 and, for b_cap <= 1023, so are their
+        // wave sums: pack two counters per 32-bit reduction
+        const bool packed = p.b_cap <= 1023;
+        const uint32_t a = wave_sum32(packed ? (n_bin | (n_bout << 16)) : n_bin);
+        const uint32_t b = wave_sum32(packed ? (n_pl | (n_drop << 16)) : n_bout);
+        const uint32_t c = packed ? 0u : wave_sum32(n_pl | (n_drop << 16));
         if ((threadIdx.x & 63) == 0) {
-            if (a) atomicAdd(stats + ASTRO_STAT_BULLETS_IN, (unsigned long long)a);
-            if (b) atomicAdd(stats + ASTRO_STAT_BULLETS_OUT, (unsigned long long)b);
-            if (c) atomicAdd(stats + ASTRO_STAT_RESETS, (unsigned long long)c);
-            if (d) atomicAdd(stats + ASTRO_STAT_COLLISIONS, (unsigned long long)d);
-            if (e) atomicAdd(stats + ASTRO_STAT_TIMEOUTS, (unsigned long long)e);
-            if (f) atomicAdd(stats + ASTRO_STAT_OVERFLOWS, (unsigned long long)f);
-            if (g) atomicAdd(stats + ASTRO_STAT_PLANETS, (unsigned long long)g);
+            unsigned long long *slot = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * ASTRO_NSTATS;
+            const uint64_t bin = packed ? (a & 0xffff) : a;
+            const uint64_t bout = packed ? (a >> 16) : b;
+            const uint64_t pl = packed ? (b & 0xffff) : (c & 0xffff);
+            const uint64_t drop = packed ? (b >> 16) : (c >> 16);
+            if (bin) atomicAdd(slot + ASTRO_STAT_BULLETS_IN, (unsigned long long)bin);
+            if (bout) atomicAdd(slot + ASTRO_STAT_BULLETS_OUT, (unsigned long long)bout);
+            if (m_reset) atomicAdd(slot + ASTRO_STAT_RESETS, (unsigned long long)__popcll(m_reset));
+            if (m_coll) atomicAdd(slot + ASTRO_STAT_COLLISIONS, (unsigned long long)__popcll(m_coll));
+            if (m_tout) atomicAdd(slot + ASTRO_STAT_TIMEOUTS, (unsigned long long)__popcll(m_tout));
+            if (drop) atomicAdd(slot + ASTRO_STAT_OVERFLOWS, (unsigned long long)drop);
+            if (pl) atomicAdd(slot + ASTRO_STAT_PLANETS, (unsigned long long)pl);
         }
     }
 }

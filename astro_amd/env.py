@@ -81,7 +81,7 @@ class BatchedEnv:
         self.stream = z(N, 4, dt=torch.int32)
         self.reward = z(N, S, dt=torch.float32)
         self.done = z(N, dt=torch.uint8)
-        self.stats = z(_lib.NSTATS, dt=torch.int64)
+        self.stats = z(max(1, (N + 63) // 64), _lib.NSTATS, dt=torch.int64)
         self.fire_bits = torch.from_numpy(self.schedule.fire_bits().view(np.int32)).to(dev)
 
         k = _schedule.kernel_constants(config)
@@ -178,7 +178,7 @@ class BatchedEnv:
             bullets=self.bullets.permute(1, 0, 2), nbullets=self.nbullets, tick=self.tick)
 
     def stat_dict(self):
-        v = self.stats.cpu().tolist()
+        v = self.stats.sum(0).cpu().tolist()
         return dict(zip(_lib.STAT_NAMES, v))
 
     # ----------------------------------------------------- host import/export

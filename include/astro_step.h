@@ -80,8 +80,11 @@ typedef struct AstroState {
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
 } AstroState;
 
-/* Statistics accumulated by astro_step when `stats` is non-NULL
- * (uint64 device counters, added to, never cleared by the library). */
+/* Statistics accumulated by astro_step when `stats` is non-NULL: uint64
+ * [ceil(n_env / 64)][ASTRO_NSTATS], one private row per wave64 (env block
+ * 64*w .. 64*w+63), added to and never cleared by the library.  Sum the rows
+ * for totals.  (A private row per wave keeps the counters contention-free:
+ * every wave adding into one shared row serialises at the memory side.) */
 enum {
     ASTRO_STAT_BULLETS_IN = 0,  /* live bullets read */
     ASTRO_STAT_BULLETS_OUT = 1, /* live bullets written */

@@ -129,17 +129,21 @@ def test_shard_ranges_partition(n, world):
 
 
 def test_wrap_formula_matches_numpy_remainder():
-    """The kernel's wrap (fmod, +2 if negative, +0 if zero, -1) equals numpy's
+    """The kernel's wrap (x - 2 trunc(x/2), +2 if negative, +0 if zero, -1) equals numpy's
     ((x + 1) % 2) - 1 (util.py:148) on random and edge values."""
     rng = np.random.default_rng(5)
     x = np.concatenate([rng.uniform(-3, 3, 100000), rng.uniform(-1e-15, 1e-15, 1000),
                         [-1.0, 1.0, 3.0, -3.0, 0.0, -0.0, 1 - 2 ** -53, -1 + 2 ** -53, 2.0 ** -1074]])
-    m = np.fmod(x + 1.0, 2.0)
-    m = np.where(m != 0, np.where(m < 0, m + 2.0, m), 0.0)
+    v = x + 1.0
+    m = v - 2.0 * np.trunc(v * 0.5)
+    m = np.where(m < 0, m + 2.0, m)
+    m = np.where(m == 0, 0.0, m)
     mine = m - 1.0
     ref = ((x + 1) % 2) - 1
     assert (mine.view(np.int64) == ref.view(np.int64)).all()
     x32 = x.astype(np.float32)
-    m = np.fmod(x32 + np.float32(1), np.float32(2))
-    m = np.where(m != 0, np.where(m < 0, m + np.float32(2), m), np.float32(0)).astype(np.float32)
+    v = x32 + np.float32(1)
+    m = v - np.float32(2) * np.trunc(v * np.float32(0.5))
+    m = np.where(m < 0, m + np.float32(2), m).astype(np.float32)
+    m = np.where(m == 0, np.float32(0), m).astype(np.float32)
     assert ((m - np.float32(1)).view(np.int32) == (((x32 + 1) % 2) - 1).view(np.int32)).all()

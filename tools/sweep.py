@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Kernel-time sweep (HIP events per launch) over env count and features.
+
+Diagnostic tool for the GPU box: prints one JSON line per variant with the
+mean/median astro_step kernel time, env-steps/s of the kernel alone and the
+steady-state stats.  All variants run interleaved-free but in ONE process
+(same device, same clocks)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from astro_amd import BatchedEnv, DEFAULT_CONFIG  # noqa: E402
+import bench  # noqa: E402
+
+
+def run(name, cfg, n, ticks=200, warm=150, b_cap=32, p_pad=4, auto_reset=True, stats=True,
+        dtype=torch.float32):
+    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, dtype=dtype,
+                     auto_reset=auto_reset)
+    env.reset()
+    ctl = torch.from_numpy(bench.controls(0, n, env.S, warm + ticks)).cuda()
+    for t in range(warm):
+        env.launch(ctl[t].data_ptr(), stats=stats)
+    torch.cuda.synchronize()
+    s0 = env.stat_dict()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(ticks)]
+    st = torch.cuda.current_stream()
+    for k in range(ticks):
+        evs[k][0].record(st)
+        env.launch(ctl[warm + k].data_ptr(), stats=stats)
+        evs[k][1].record(st)
+    torch.cuda.synchronize()
+    ms = np.array([a.elapsed_time(b) for a, b in evs])
+    s1 = env.stat_dict()
+    d = {k: (s1[k] - s0[k]) / ticks for k in s0}
+    print(json.dumps(dict(name=name, n=n, mean_us=ms.mean() * 1e3, med_us=float(np.median(ms)) * 1e3,
+                          min_us=ms.min() * 1e3, env_steps_per_s=n / (ms.mean() * 1e-3),
+                          bullets_per_env=d['bullets_in'] / n, resets=d['resets'],
+                          planets_per_env=d['planets'] / n)), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--set', default='basic')
+    a = ap.parse_args()
+    D = DEFAULT_CONFIG
+    if a.set == 'basic':
+        for n in (16384, 65536, 262144, 1048576):
+            run('c3', D, n)
+        run('c3_nostats', D, 65536, stats=False)
+        run('c3_noreset', D, 65536, auto_reset=False)
+        run('c2_nobullets', D._replace(reload_time=1000), 65536)
+        run('c2_nobullets_noreset', D._replace(reload_time=1000), 65536, auto_reset=False)
+        run('c3_f64', D, 65536, dtype=torch.float64)
+        run('c5', D._replace(max_planets=8), 131072, p_pad=8)
+
+
+if __name__ == '__main__':
+    main()
