@@ -220,16 +220,34 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     return y;
 }
 
+// key[to] of init_genrand given key[from] = v: the 397-step sequential chain
+// every RandomState(seed) pays before its first output
+__device__ __forceinline__ uint32_t mt_key_at(uint32_t v, uint32_t from, uint32_t to) {
+    for (uint32_t k = from + 1; k <= to; ++k) v = mt_key_next(v, k);
+    return v;
+}
+
+constexpr uint32_t MT_PROLOGUE = 397;
+// Amortised seeding: every running env advances the init chain of its NEXT
+// game's seed by this many steps per tick, so a game that ends after
+// >= 397/8 = 50 ticks re-creates without paying the chain (a wave otherwise
+// stalls on whichever of its 64 games ended).
+constexpr uint32_t MT_STEPS_PER_TICK = 8;
+
+// hdr word 0 = tick | pending-chain progress << 22
+constexpr int TICK_BITS = 22;
+constexpr uint32_t TICK_MASK = (1u << TICK_BITS) - 1;
+
 struct MTLazy {
     uint32_t a;  // key[i]
     uint32_t b;  // key[i + 397]
     uint32_t i;
 
-    __device__ void seed(uint32_t s) {
+    __device__ void seed(uint32_t s) { seed_from(s, mt_key_at(s, 0, 397)); }
+    // seed with key[397] already known (the amortised prologue below)
+    __device__ void seed_from(uint32_t s, uint32_t key397) {
         a = s;
-        uint32_t v = s;
-        for (uint32_t k = 1; k <= 397; ++k) v = mt_key_next(v, k);
-        b = v;
+        b = key397;
         i = 0;
     }
     __device__ bool ok() const { return i < 227; }
@@ -274,8 +292,8 @@ constexpr double PI = 3.141592653589793;      // np.pi
 // create() (core.py:86-135) for env i from `seed`; writes the env's slots.
 
 template <typename T, int S, int PMAX>
-__device__ void create_env(const AstroParams &p, const AstroState &st, int i, uint32_t seed,
-                           int &flags_out) {
+__device__ int create_env(const AstroParams &p, const AstroState &st, int i, uint32_t seed, uint32_t key397,
+                          int &flags_out) {
     using V = typename Store<T>::V;
     const size_t N = size_t(st.n_env);
     V *ships = reinterpret_cast<V *>(st.ships);
@@ -283,7 +301,7 @@ __device__ void create_env(const AstroParams &p, const AstroState &st, int i, ui
     V *planets = reinterpret_cast<V *>(st.planets);
 
     MTLazy g;
-    g.seed(seed);
+    g.seed_from(seed, key397);
     int n = g.randint(1, p.max_planets + 1);
     // outer = outer_ship_position * sign(rand(2).astype(float32) - 0.5)
     const float u0 = float(g.rand()) - 0.5f;
@@ -349,26 +367,45 @@ __device__ void create_env(const AstroParams &p, const AstroState &st, int i, ui
     }
     if (n > PMAX) n = PMAX;
     flags_out = g.ok() ? 0 : 2;
-    st.hdr[2 * i + 0] = 0;
-    st.hdr[2 * i + 1] = n;
+    return n;
 }
 
-// next config seed of env i's generate_configs stream (core.py:77-83):
-// RandomState(stream_seed).randint(1 << 30) = one masked MT word per game
-__device__ __forceinline__ uint32_t stream_next(const AstroState &st, int i, bool &exhausted) {
+// Env i's generate_configs stream (core.py:77-83): RandomState(stream_seed)
+// .randint(1 << 30) = one masked MT word per game.  The record holds the
+// cursor (key[k], key[k+397], k) and, in .w, the PENDING seed: the next game's
+// seed, drawn one game ahead so its init chain can be advanced while the
+// current game runs.  Returns the pending seed and draws its successor.
+__device__ __forceinline__ uint32_t stream_take(const AstroState &st, int i, uint32_t &next_pending,
+                                                bool &exhausted) {
     uint4 c = reinterpret_cast<uint4 *>(st.stream)[i];
+    const uint32_t pending = c.w;
     MTLazy g;
     g.a = c.x;
     g.b = c.y;
     g.i = c.z;
     exhausted = !g.ok();
-    const uint32_t seed = g.next() & ((1u << 30) - 1);
+    next_pending = g.next() & ((1u << 30) - 1);
     c.x = g.a;
     c.y = g.b;
     c.z = g.i;
-    c.w = seed;
+    c.w = next_pending;
     reinterpret_cast<uint4 *>(st.stream)[i] = c;
-    return seed;
+    return pending;
+}
+
+// Start env i's next game from its stream: finish the pending seed's chain
+// (usually already complete), create, and queue the following seed.
+template <typename T, int S, int PMAX>
+__device__ __forceinline__ void restart_from_stream(const AstroParams &p, const AstroState &st, int i,
+                                                    uint32_t pend_v, uint32_t pend_j) {
+    const uint32_t key397 = mt_key_at(pend_v, pend_j, MT_PROLOGUE);
+    bool exhausted;
+    uint32_t next_pending;
+    const uint32_t seed = stream_take(st, i, next_pending, exhausted);
+    int cf = 0;
+    const int n = create_env<T, S, PMAX>(p, st, i, seed, key397, cf);
+    const int flags = (exhausted || cf) ? 2 : 0;
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(next_pending), int(seed));
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -490,7 +527,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         V *bullets = reinterpret_cast<V *>(st.bullets);
 
         // ---- round 1 of loads: header, ships, control (independent)
-        const int2 h = reinterpret_cast<const int2 *>(st.hdr)[i];
+        const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
         double sx[S], sy[S], sdx[S], sdy[S], sb[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -509,7 +546,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         } else {
             ctl[0] = int(control[i]);
         }
-        const int tick = h.x;
+        const int tick = int(uint32_t(h.x) & TICK_MASK);
+        const uint32_t pend_j = uint32_t(h.x) >> TICK_BITS;
+        const uint32_t pend_v = uint32_t(h.z);
         int np = h.y & 0xff;
         int flags = (h.y >> 8) & 0xff;
         const int nb = int(uint32_t(h.y) >> 16);
@@ -682,18 +721,24 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                 }
             }
             if (dropped) flags |= 1;
-            reinterpret_cast<int2 *>(st.hdr)[i] = make_int2(tick + 1, np | (flags << 8) | (w << 16));
+            // advance the next game's init chain (amortised seeding)
+            uint32_t v = pend_v, j = pend_j;
+#pragma unroll
+            for (uint32_t k = 0; k < MT_STEPS_PER_TICK; ++k) {
+                if (j < MT_PROLOGUE) {
+                    ++j;
+                    v = mt_key_next(v, j);
+                }
+            }
+            reinterpret_cast<int4 *>(st.hdr)[i] =
+                make_int4(int(uint32_t(tick + 1) | (j << TICK_BITS)), np | (flags << 8) | (w << 16), int(v), h.w);
             n_bout = uint32_t(w);
             n_drop = uint32_t(dropped);
         } else {
             f_coll = collided;
             f_tout = timeout;
             if (auto_reset) {
-                bool exhausted;
-                const uint32_t seed = stream_next(st, i, exhausted);
-                int cf = 0;
-                create_env<T, S, PMAX>(p, st, i, seed, cf);
-                if (exhausted || cf) st.hdr[2 * i + 1] |= 2 << 8;
+                restart_from_stream<T, S, PMAX>(p, st, i, pend_v, pend_j);
                 f_reset = true;
             }
         }
@@ -733,12 +778,17 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= st.n_env) return;
     if (mask && !mask[i]) return;
-    bool exhausted = false;
-    const uint32_t seed = seeds ? seeds[i] : stream_next(st, i, exhausted);
+    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+    if (!seeds) {
+        restart_from_stream<T, S, PMAX>(p, st, i, uint32_t(h.z), uint32_t(h.x) >> TICK_BITS);
+        return;
+    }
+    // explicit seed: full chain now; the stream's pending game stays queued
     int cf = 0;
-    create_env<T, S, PMAX>(p, st, i, seed, cf);
-    if (exhausted || cf) st.hdr[2 * i + 1] |= 2 << 8;
-    if (seeds && st.stream) reinterpret_cast<uint32_t *>(st.stream)[4 * i + 3] = seed;
+    const uint32_t seed = seeds[i];
+    const int n = create_env<T, S, PMAX>(p, st, i, seed, mt_key_at(seed, 0, MT_PROLOGUE), cf);
+    reinterpret_cast<int4 *>(st.hdr)[i] =
+        make_int4(int(uint32_t(h.x) & ~TICK_MASK), n | ((cf ? 2 : 0) << 8), h.z, int(seed));
 }
 
 __global__ __launch_bounds__(BLOCK) void astro_stream_init_kernel(AstroState st,
@@ -747,7 +797,9 @@ __global__ __launch_bounds__(BLOCK) void astro_stream_init_kernel(AstroState st,
     if (i >= st.n_env) return;
     MTLazy g;
     g.seed(seeds[i]);
-    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, 0u);
+    const uint32_t first = g.next() & ((1u << 30) - 1);   // game 0's seed, pending
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, first);
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, 1, int(first), 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -773,7 +825,7 @@ int check_state(const AstroState *s) {
         return fail(-4, "a state array is NULL");
     if (!aligned16(s->ships) || !aligned16(s->planets) || !aligned16(s->bullets))
         return fail(-5, "ships/planets/bullets must be 16-byte aligned");
-    if ((reinterpret_cast<uintptr_t>(s->hdr) & 7u) != 0) return fail(-5, "hdr must be 8-byte aligned");
+    if ((reinterpret_cast<uintptr_t>(s->hdr) & 15u) != 0) return fail(-5, "hdr must be 16-byte aligned");
     if (s->state_f64 != 0 && s->state_f64 != 1) return fail(-6, "state_f64 must be 0 or 1");
     return 0;
 }
@@ -786,7 +838,7 @@ int check_params(const AstroParams *p) {
     if (p->max_planets < 1 || p->max_planets > p->p_pad)
         return fail(-14, "max_planets must be in [1, p_pad]");
     if (p->b_cap < 1 || p->b_cap > 65535) return fail(-15, "b_cap must be in [1, 65535]");
-    if (p->timeout_tick < 0) return fail(-16, "timeout_tick < 0");
+    if (p->timeout_tick < 0 || p->timeout_tick >= int(TICK_MASK)) return fail(-16, "timeout_tick out of [0, 2^22)");
     if (p->timeout_tick > 0 && !p->fire_bits) return fail(-17, "fire_bits is NULL");
     return 0;
 }
@@ -883,6 +935,7 @@ int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *s
     if (s->n_env == 0) return 0;
     if (!s->stream || !stream_seeds) return fail(-41, "stream / stream_seeds is NULL");
     if (reinterpret_cast<uintptr_t>(s->stream) & 15u) return fail(-5, "stream must be 16-byte aligned");
+    if (!s->hdr || (reinterpret_cast<uintptr_t>(s->hdr) & 15u)) return fail(-5, "hdr must be 16-byte aligned");
     const int grid = (s->n_env + BLOCK - 1) / BLOCK;
     hipLaunchKernelGGL(astro_stream_init_kernel, dim3(grid), dim3(BLOCK), 0,
                        reinterpret_cast<hipStream_t>(stream), *s, stream_seeds);

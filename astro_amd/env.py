@@ -14,8 +14,9 @@ All state lives in HBM as PyTorch tensors, struct-of-arrays, entity-major:
 
     ships    [S, N, 4]   x, y, dx, dy        ships_b  [S, N]
     planets  [P, N, 4]   x, y, dx, dy        bullets  [B, N, 4]
-    hdr      [N, 2]      tick, nplanets | flags << 8 | nbullets << 16
-    stream   [N, 4]      seed-stream cursor + current game seed
+    hdr      [N, 4]      tick | chain << 22, nplanets | flags << 8 | nbullets << 16,
+                         next game's init-chain value, current game seed
+    stream   [N, 4]      seed-stream cursor + next game's seed
 
 and every call goes through libastro_hip.so (include/astro_step.h) on the
 current torch stream.  There is no CPU path.
@@ -29,6 +30,8 @@ import torch
 from . import _lib
 from .config import Bodies, State, nships as _nships
 from . import schedule as _schedule
+
+TICK_MASK = (1 << 22) - 1
 
 Observation = collections.namedtuple(
     'Observation', ('ships', 'ships_b', 'planets', 'nplanets', 'bullets', 'nbullets', 'tick'))
@@ -77,7 +80,7 @@ class BatchedEnv:
         self.ships_b = z(S, N)
         self.planets = z(self.p_pad, N, 4)
         self.bullets = z(self.b_cap, N, 4)
-        self.hdr = z(N, 2, dt=torch.int32)
+        self.hdr = z(N, 4, dt=torch.int32)
         self.stream = z(N, 4, dt=torch.int32)
         self.reward = z(N, S, dt=torch.float32)
         self.done = z(N, dt=torch.uint8)
@@ -152,7 +155,7 @@ class BatchedEnv:
 
     @property
     def tick(self):
-        return self.hdr[:, 0]
+        return self.hdr[:, 0] & TICK_MASK
 
     @property
     def nplanets(self):
@@ -168,7 +171,8 @@ class BatchedEnv:
 
     @property
     def game_seed(self):
-        return self.stream[:, 3]
+        """Config.seed of each env's current game."""
+        return self.hdr[:, 3]
 
     def obs(self):
         """Env-major views of the state (no copies): ships [N, S, 4] ..."""
@@ -211,9 +215,11 @@ class BatchedEnv:
         nb = np.asarray(nbullets, dtype=np.int64)
         if (nb > self.b_cap).any():
             raise ValueError('a state holds more bullets than b_cap')
-        hdr = np.stack([np.asarray(tick, np.int64),
-                        np.asarray(nplanets, np.int64) | (nb << 16)], -1)
-        self.hdr.copy_(torch.as_tensor(hdr.astype(np.int64).astype(np.uint32).view(np.int32)).to(dev))
+        old = self.hdr.cpu().numpy().view(np.uint32).astype(np.int64)
+        hdr = old.copy()
+        hdr[:, 0] = (old[:, 0] & ~TICK_MASK) | np.asarray(tick, np.int64)
+        hdr[:, 1] = np.asarray(nplanets, np.int64) | (nb << 16)
+        self.hdr.copy_(torch.as_tensor(hdr.astype(np.uint32).view(np.int32)).to(dev))
 
     def state_of(self, i, host=None):
         """Reference-shaped State of env i (numpy, reference dtypes: float32

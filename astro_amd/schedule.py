@@ -13,7 +13,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-TICK_LIMIT = 1 << 24
+TICK_LIMIT = (1 << 22) - 1   # tick shares hdr word 0 with 10 bits of chain progress
 
 
 @dataclass

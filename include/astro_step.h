@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 1
+#define ASTRO_ABI_VERSION 2
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -65,17 +65,21 @@ typedef struct AstroParams {
 } AstroParams;
 
 /* Per-env state arrays (device pointers).  hdr packs
- *   hdr[2*i+0] = tick (steps since create)
- *   hdr[2*i+1] = nplanets | flags << 8 | nbullets << 16
+ *   hdr[4*i+0] = tick (steps since create, < 2^22) | chain progress j << 22
+ *   hdr[4*i+1] = nplanets | flags << 8 | nbullets << 16
+ *   hdr[4*i+2] = key[j] of the NEXT game's MT19937 init chain (see stream)
+ *   hdr[4*i+3] = the current game's seed (its Config.seed)
  * flags: bit0 = a bullet was dropped (b_cap full) this game,
- *        bit1 = the env's seed stream ran past its 227 exact games. */
+ *        bit1 = the env's seed stream ran past its 227 exact games.
+ * Every running env advances its next game's 397-step init chain by 8 steps
+ * per tick, so an auto-reset normally starts with the chain complete. */
 typedef struct AstroState {
     void *ships;        /* [nships][n_env][4]  x, y, dx, dy */
     void *ships_b;      /* [nships][n_env]     bearing */
     void *planets;      /* [p_pad][n_env][4]   x, y, dx, dy */
     void *bullets;      /* [b_cap][n_env][4]   x, y, dx, dy */
-    int32_t *hdr;       /* [n_env][2] */
-    uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, game seed */
+    int32_t *hdr;       /* [n_env][4], 16-byte aligned */
+    uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, next game's seed */
     int32_t n_env;
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
 } AstroState;
@@ -113,7 +117,8 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
 int astro_reset(const AstroParams *p, const AstroState *s, const uint32_t *seeds,
                 const uint8_t *mask, void *stream);
 
-/* Position env i's seed stream at generate_configs(seed=stream_seeds[i]). */
+/* Position env i's seed stream at generate_configs(seed=stream_seeds[i]) and
+ * queue its first game (the next astro_reset without seeds creates it). */
 int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *stream);
 
 #ifdef __cplusplus
