@@ -144,6 +144,29 @@ __device__ __forceinline__ double dist2(double ax, double ay, double bx, double 
     return double(dx * dx + dy * dy);
 }
 
+// Collision test |a - b|^2 < r2 of _collisions (core.py:210-212), exact.
+// At tick 0 the reference evaluates the distance in float32 (create's
+// float32 arrays) and that float32 value is the answer.  Later it uses
+// float64: the float32 distance of the same inputs is within ~3e-7
+// relative (well inside the 1e-4 guard, which also covers float64 state
+// rounded to float32), so only a distance inside the guard band pays the
+// float64 recomputation.
+__device__ __forceinline__ bool closer(double ax, double ay, double bx, double by, double r2, float r2_lo,
+                                       float r2_hi, bool t0) {
+    const float dx = float(ax) - float(bx);
+    const float dy = float(ay) - float(by);
+    const float d2 = dx * dx + dy * dy;
+    if (t0) return double(d2) < r2;
+    if (d2 < r2_lo) return true;
+    if (d2 > r2_hi) return false;
+    return dist2<double>(ax, ay, bx, by) < r2;
+}
+
+struct Guard {
+    float lo, hi;
+    __device__ explicit Guard(double r2) : lo(float(r2 * (1.0 - 1e-4))), hi(float(r2 * (1.0 + 1e-4))) {}
+};
+
 // Planet-on-planet gravity (core.py:291) for every planet i < np, in the
 // reference's summation order (j = 0..np-1, self term +0.0 included).  The
 // pair (i, j) and (j, i) share d2 bit for bit and their terms are exact
@@ -352,7 +375,9 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
         const int reverse = g.randint(0, 2) == 0 ? -1 : 1;
         const double amp = sqrt(p.gravity * p.planet_mass * double(n - 1) / 2.0);
         const double turn = double(reverse) * PI / 2.0;
-        for (int j = 0; j < n && j < PMAX; ++j) {
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+            if (j >= n) continue;
             const double orient = base + double(j) * stp;
             float ps, pc, vs, vc;
             np_sincosf(float(orient), ps, pc);
@@ -371,41 +396,30 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
 }
 
 // Env i's generate_configs stream (core.py:77-83): RandomState(stream_seed)
-// .randint(1 << 30) = one masked MT word per game.  The record holds the
-// cursor (key[k], key[k+397], k) and, in .w, the PENDING seed: the next game's
-// seed, drawn one game ahead so its init chain can be advanced while the
-// current game runs.  Returns the pending seed and draws its successor.
-__device__ __forceinline__ uint32_t stream_take(const AstroState &st, int i, uint32_t &next_pending,
-                                                bool &exhausted) {
-    uint4 c = reinterpret_cast<uint4 *>(st.stream)[i];
-    const uint32_t pending = c.w;
+// .randint(1 << 30) = one masked MT word per game.  The stream record holds
+// the cursor (key[k], key[k+397], k) and the CURRENT game's seed; the next
+// game's seed is drawn one game ahead and lives in hdr (.w) with its
+// partially advanced init chain (.z, progress in .x >> 22), so a reset can
+// start creating before the cold stream record arrives.
+
+// Start env i's next game: finish the pending seed's chain (usually done
+// already), create, draw the seed after it.
+template <typename T, int S, int PMAX>
+__device__ __forceinline__ void restart_from_stream(const AstroParams &p, const AstroState &st, int i,
+                                                    uint32_t pend_v, uint32_t pend_j, uint32_t pend_seed) {
+    uint4 c = reinterpret_cast<uint4 *>(st.stream)[i];   // in flight during create
+    const uint32_t key397 = mt_key_at(pend_v, pend_j, MT_PROLOGUE);
+    int cf = 0;
+    const int n = create_env<T, S, PMAX>(p, st, i, pend_seed, key397, cf);
     MTLazy g;
     g.a = c.x;
     g.b = c.y;
     g.i = c.z;
-    exhausted = !g.ok();
-    next_pending = g.next() & ((1u << 30) - 1);
-    c.x = g.a;
-    c.y = g.b;
-    c.z = g.i;
-    c.w = next_pending;
-    reinterpret_cast<uint4 *>(st.stream)[i] = c;
-    return pending;
-}
-
-// Start env i's next game from its stream: finish the pending seed's chain
-// (usually already complete), create, and queue the following seed.
-template <typename T, int S, int PMAX>
-__device__ __forceinline__ void restart_from_stream(const AstroParams &p, const AstroState &st, int i,
-                                                    uint32_t pend_v, uint32_t pend_j) {
-    const uint32_t key397 = mt_key_at(pend_v, pend_j, MT_PROLOGUE);
-    bool exhausted;
-    uint32_t next_pending;
-    const uint32_t seed = stream_take(st, i, next_pending, exhausted);
-    int cf = 0;
-    const int n = create_env<T, S, PMAX>(p, st, i, seed, key397, cf);
+    const bool exhausted = !g.ok();
+    const uint32_t next_seed = g.next() & ((1u << 30) - 1);
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, pend_seed);
     const int flags = (exhausted || cf) ? 2 : 0;
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(next_pending), int(seed));
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(next_seed), int(next_seed));
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -416,6 +430,25 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 
 // ---------------------------------------------------------------------------
 // the step kernel
+
+// Diagnostic build only (-DASTRO_STAMPS, tools/sweep.py --stamps): s_memtime
+// at section boundaries, lane 0 stores them over the stats rows.  Never in
+// the shipped library.
+#ifdef ASTRO_STAMPS
+#define STAMP(k)                                                                         \
+    do {                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        unsigned long long t_;                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        stamp_[k] = t_;                                                                  \
+    } while (0)
+constexpr int NSTAMP = 16;
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
 
 constexpr int BLOCK = 64;
 constexpr int BCHUNK = 8;  // bullets loaded per batch: 8 loads in flight per lane
@@ -429,34 +462,38 @@ template <typename C, typename T, int S, int PMAX>
 __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store<T>::V *bullets, size_t NN, int i,
                                             int nb, int np, const double (&px)[PMAX], const double (&py)[PMAX],
                                             const double (&sx)[S], const double (&sy)[S],
-                                            typename Store<T>::V (&buf)[BCHUNK], bool (&hit)[S], int &w,
-                                            int &dropped) {
+                                            typename Store<T>::V (&cur)[BCHUNK], bool (&hit)[S], int &w,
+                                            int &dropped, bool t0) {
     using V = typename Store<T>::V;
     const C dt = C(p.dt);
+    const Guard gp(p.r2_p0), gs(p.r2_s0);
     for (int base = 0; base < nb; base += BCHUNK) {
-        if (base > 0) {
+        // prefetch the next chunk before working on this one (slots read
+        // ahead are never below the write cursor: w <= slot being read)
+        V nxt[BCHUNK];
+        if (base + BCHUNK < nb) {
 #pragma unroll
             for (int u = 0; u < BCHUNK; ++u) {
-                const int k = base + u < nb ? base + u : 0;
-                buf[u] = bullets[size_t(k) * NN + i];
+                const int k = base + BCHUNK + u < nb ? base + BCHUNK + u : 0;
+                nxt[u] = bullets[size_t(k) * NN + i];
             }
         }
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) {
             if (base + u < nb) {
-                const double x = double(buf[u].x), y = double(buf[u].y);
+                const double x = double(cur[u].x), y = double(cur[u].y);
                 bool bh = false;
 #pragma unroll
                 for (int j = 0; j < PMAX; ++j)
-                    if (j < np) bh = bh || dist2<C>(x, y, px[j], py[j]) < p.r2_p0;
+                    if (j < np) bh = bh || closer(x, y, px[j], py[j], p.r2_p0, gp.lo, gp.hi, t0);
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
-                    const bool hs = dist2<C>(x, y, sx[s], sy[s]) < p.r2_s0;
+                    const bool hs = closer(x, y, sx[s], sy[s], p.r2_s0, gs.lo, gs.hi, t0);
                     bh = bh || hs;
                     hit[s] = hit[s] || hs;
                 }
                 if (!bh) {
-                    const C ndx = C(buf[u].z) + C(0), ndy = C(buf[u].w) + C(0);
+                    const C ndx = C(cur[u].z) + C(0), ndy = C(cur[u].w) + C(0);
                     const C nx = C(x) + dt * ndx, ny = C(y) + dt * ndy;
                     const bool keep = (C(-1) <= nx && nx <= C(1)) || (C(-1) <= ny && ny <= C(1));
                     const bool fits = w < p.b_cap;
@@ -476,6 +513,8 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
                 }
             }
         }
+#pragma unroll
+        for (int u = 0; u < BCHUNK; ++u) cur[u] = nxt[u];
     }
 }
 
@@ -518,6 +557,10 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
     const bool active = i < N;
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
     bool f_reset = false, f_coll = false, f_tout = false;
+#ifdef ASTRO_STAMPS
+    unsigned long long stamp_[NSTAMP] = {};
+#endif
+    STAMP(0);
 
     if (active) {
         const size_t NN = size_t(N);
@@ -555,6 +598,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
         const bool live = tick < p.timeout_tick;
         const bool t0 = tick == 0;
+        STAMP(1);
 
         // ---- round 2 (needs the header): planets (padded slots re-read
         //      slot 0), the fire word, the first bullet chunk
@@ -599,37 +643,36 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             dbear[s] = p.db * double((ctl[s] >> 1) - 1);
         }
 
+        STAMP(2);
         // ---- collisions on the old state (core.py:241-253): ships vs
         //      ships/planets here, ships/planets vs bullets in the bullet pass
         bool hit[S];
+        {
+            const Guard gsp(p.r2_sp), gss(p.r2_ss);
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-            bool hs = false;
+            for (int s = 0; s < S; ++s) {
+                bool hs = false;
 #pragma unroll
-            for (int j = 0; j < PMAX; ++j) {
-                if (j < np) {
-                    const double d2 = t0 ? dist2<float>(sx[s], sy[s], px[j], py[j])
-                                         : dist2<double>(sx[s], sy[s], px[j], py[j]);
-                    hs = hs || d2 < p.r2_sp;
-                }
+                for (int j = 0; j < PMAX; ++j)
+                    if (j < np) hs = hs || closer(sx[s], sy[s], px[j], py[j], p.r2_sp, gsp.lo, gsp.hi, t0);
+                hit[s] = hs;
             }
-            hit[s] = hs;
-        }
-        if (S == 2) {
-            const double d2 = t0 ? dist2<float>(sx[0], sy[0], sx[S - 1], sy[S - 1])
-                                 : dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]);
-            const bool hh = d2 < p.r2_ss;
-            hit[0] = hit[0] || hh;
-            hit[S - 1] = hit[S - 1] || hh;
+            if (S == 2) {
+                const bool hh = closer(sx[0], sy[0], sx[S - 1], sy[S - 1], p.r2_ss, gss.lo, gss.hi, t0);
+                hit[0] = hit[0] || hh;
+                hit[S - 1] = hit[S - 1] || hh;
+            }
         }
 
+        STAMP(3);
         // ---- bullets
         int w = 0, dropped = 0;
         if (t0)
-            bullet_pass<float, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped);
+            bullet_pass<float, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, true);
         else
-            bullet_pass<double, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped);
+            bullet_pass<double, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, false);
         n_bin = uint32_t(nb);
+        STAMP(4);
 
         const bool collided = S == 2 ? (hit[0] || hit[S - 1]) : hit[0];
         const bool timeout = !collided && !live;
@@ -646,6 +689,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             reward[i] = rw[0];
         }
         done_out[i] = done;
+        STAMP(5);
 
         if (!done) {
             // ---- fire from the OLD ship state, after the survivors (core.py:267-280)
@@ -673,6 +717,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                 ships_b[size_t(s) * NN + i] = T(sb[s] + dbear[s]);
             }
 
+            STAMP(6);
             // ---- planets: mutual gravity (core.py:289-294); float32 at tick 0
             //      (create's float32 positions) and for a lone planet (its
             //      arrays stay float32 for the whole game)
@@ -720,6 +765,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                     }
                 }
             }
+            STAMP(7);
             if (dropped) flags |= 1;
             // advance the next game's init chain (amortised seeding)
             uint32_t v = pend_v, j = pend_j;
@@ -732,17 +778,29 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             }
             reinterpret_cast<int4 *>(st.hdr)[i] =
                 make_int4(int(uint32_t(tick + 1) | (j << TICK_BITS)), np | (flags << 8) | (w << 16), int(v), h.w);
+
             n_bout = uint32_t(w);
             n_drop = uint32_t(dropped);
+            STAMP(8);
         } else {
+            STAMP(9);
             f_coll = collided;
             f_tout = timeout;
             if (auto_reset) {
-                restart_from_stream<T, S, PMAX>(p, st, i, pend_v, pend_j);
+                restart_from_stream<T, S, PMAX>(p, st, i, pend_v, pend_j, uint32_t(h.w));
                 f_reset = true;
             }
+            STAMP(10);
         }
     }
+    STAMP(11);
+#ifdef ASTRO_STAMPS
+    if (stats && (threadIdx.x & 63) == 0) {
+        unsigned long long *row = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * NSTAMP;
+        for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
+    }
+    return;
+#endif
 
     // ---- statistics: one private slot per wave (contention-free no-return
     //      atomics; summed over slots by the host)
@@ -780,7 +838,7 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
     if (mask && !mask[i]) return;
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
     if (!seeds) {
-        restart_from_stream<T, S, PMAX>(p, st, i, uint32_t(h.z), uint32_t(h.x) >> TICK_BITS);
+        restart_from_stream<T, S, PMAX>(p, st, i, uint32_t(h.z), uint32_t(h.x) >> TICK_BITS, uint32_t(h.w));
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued
@@ -788,7 +846,8 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
     const uint32_t seed = seeds[i];
     const int n = create_env<T, S, PMAX>(p, st, i, seed, mt_key_at(seed, 0, MT_PROLOGUE), cf);
     reinterpret_cast<int4 *>(st.hdr)[i] =
-        make_int4(int(uint32_t(h.x) & ~TICK_MASK), n | ((cf ? 2 : 0) << 8), h.z, int(seed));
+        make_int4(int(uint32_t(h.x) & ~TICK_MASK), n | ((cf ? 2 : 0) << 8), h.z, h.w);
+    if (st.stream) reinterpret_cast<uint32_t *>(st.stream)[4 * i + 3] = seed;
 }
 
 __global__ __launch_bounds__(BLOCK) void astro_stream_init_kernel(AstroState st,
@@ -798,8 +857,8 @@ __global__ __launch_bounds__(BLOCK) void astro_stream_init_kernel(AstroState st,
     MTLazy g;
     g.seed(seeds[i]);
     const uint32_t first = g.next() & ((1u << 30) - 1);   // game 0's seed, pending
-    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, first);
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, 1, int(first), 0);
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, 0u);
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, 1, int(first), int(first));
 }
 
 // ---------------------------------------------------------------------------

@@ -15,8 +15,8 @@ All state lives in HBM as PyTorch tensors, struct-of-arrays, entity-major:
     ships    [S, N, 4]   x, y, dx, dy        ships_b  [S, N]
     planets  [P, N, 4]   x, y, dx, dy        bullets  [B, N, 4]
     hdr      [N, 4]      tick | chain << 22, nplanets | flags << 8 | nbullets << 16,
-                         next game's init-chain value, current game seed
-    stream   [N, 4]      seed-stream cursor + next game's seed
+                         next game's init-chain value, next game's seed
+    stream   [N, 4]      seed-stream cursor + current game's seed
 
 and every call goes through libastro_hip.so (include/astro_step.h) on the
 current torch stream.  There is no CPU path.
@@ -172,7 +172,7 @@ class BatchedEnv:
     @property
     def game_seed(self):
         """Config.seed of each env's current game."""
-        return self.hdr[:, 3]
+        return self.stream[:, 3]
 
     def obs(self):
         """Env-major views of the state (no copies): ships [N, S, 4] ..."""

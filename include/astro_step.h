@@ -67,8 +67,8 @@ typedef struct AstroParams {
 /* Per-env state arrays (device pointers).  hdr packs
  *   hdr[4*i+0] = tick (steps since create, < 2^22) | chain progress j << 22
  *   hdr[4*i+1] = nplanets | flags << 8 | nbullets << 16
- *   hdr[4*i+2] = key[j] of the NEXT game's MT19937 init chain (see stream)
- *   hdr[4*i+3] = the current game's seed (its Config.seed)
+ *   hdr[4*i+2] = key[j] of the NEXT game's MT19937 init chain
+ *   hdr[4*i+3] = the NEXT game's seed (drawn one game ahead from the stream)
  * flags: bit0 = a bullet was dropped (b_cap full) this game,
  *        bit1 = the env's seed stream ran past its 227 exact games.
  * Every running env advances its next game's 397-step init chain by 8 steps
@@ -79,7 +79,7 @@ typedef struct AstroState {
     void *planets;      /* [p_pad][n_env][4]   x, y, dx, dy */
     void *bullets;      /* [b_cap][n_env][4]   x, y, dx, dy */
     int32_t *hdr;       /* [n_env][4], 16-byte aligned */
-    uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, next game's seed */
+    uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, current game's seed */
     int32_t n_env;
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
 } AstroState;

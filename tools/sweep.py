@@ -47,11 +47,51 @@ def run(name, cfg, n, ticks=200, warm=150, b_cap=32, p_pad=4, auto_reset=True, s
                           planets_per_env=d['planets'] / n)), flush=True)
 
 
+def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4):
+    """Per-section cycle shares from the -DASTRO_STAMPS diagnostic library."""
+    from astro_amd import _lib
+    _lib._lib = None
+    _lib.load(os.path.join(ROOT, 'astro_amd', 'libastro_hip_stamps.so'))
+    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad)
+    env.reset()
+    nw = (n + 63) // 64
+    env.stats = torch.zeros(nw, 16, dtype=torch.int64, device='cuda')
+    ctl = torch.from_numpy(bench.controls(0, n, env.S, warm + ticks)).cuda()
+    for t in range(warm):
+        env.launch(ctl[t].data_ptr(), stats=False)
+    rows = []
+    for t in range(ticks):
+        env.stats.zero_()
+        env.launch(ctl[warm + t].data_ptr(), stats=True)
+        torch.cuda.synchronize()
+        rows.append(env.stats.cpu().numpy().astype(np.int64))
+    S = np.concatenate(rows, 0)
+    s0 = S[:, 0]
+    tot = S[:, 11] - s0
+    out = dict(name=name, n=n, wave_cycles_mean=float(tot.mean()), wave_cycles_max=float(tot.max()))
+    def seg(a, b):
+        ok = (S[:, a] > 0) & (S[:, b] > 0)
+        return float((S[ok, b] - S[ok, a]).mean()) if ok.any() else None, float(ok.mean())
+    for key, (a, b) in dict(hdr_wait=(0, 1), loads2_sincos_gravity=(1, 2), ship_collide=(2, 3),
+                            bullets=(3, 4), reward=(4, 5), spawn_ships=(5, 6), planets=(6, 7),
+                            chain_hdr=(7, 8), reset=(9, 10)).items():
+        out[key] = seg(a, b)
+    out['branches_total'] = float((S[:, 11] - S[:, 5]).mean())
+    out['start_skew'] = float(s0.max() - s0.min())
+    print(json.dumps(out), flush=True)
+    _lib._lib = None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--set', default='basic')
     a = ap.parse_args()
     D = DEFAULT_CONFIG
+    if a.set == 'stamps':
+        stamps('c3', D, 65536)
+        stamps('c2', D._replace(reload_time=1000), 65536)
+        stamps('c3_16k', D, 16384)
+        return
     if a.set == 'basic':
         for n in (16384, 65536, 262144, 1048576):
             run('c3', D, n)
