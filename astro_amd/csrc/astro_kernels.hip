@@ -144,28 +144,34 @@ __device__ __forceinline__ double dist2(double ax, double ay, double bx, double 
     return double(dx * dx + dy * dy);
 }
 
-// Collision test |a - b|^2 < r2 of _collisions (core.py:210-212), exact.
-// At tick 0 the reference evaluates the distance in float32 (create's
-// float32 arrays) and that float32 value is the answer.  Later it uses
-// float64: the float32 distance of the same inputs is within ~3e-7
-// relative (well inside the 1e-4 guard, which also covers float64 state
-// rounded to float32), so only a distance inside the guard band pays the
-// float64 recomputation.
-__device__ __forceinline__ bool closer(double ax, double ay, double bx, double by, double r2, float r2_lo,
-                                       float r2_hi, bool t0) {
-    const float dx = float(ax) - float(bx);
-    const float dy = float(ay) - float(by);
-    const float d2 = dx * dx + dy * dy;
-    if (t0) return double(d2) < r2;
-    if (d2 < r2_lo) return true;
-    if (d2 > r2_hi) return false;
-    return dist2<double>(ax, ay, bx, by) < r2;
-}
-
+// Collision test |a - b|^2 < r2 of _collisions (core.py:210-212), exact,
+// branch-free.  At tick 0 the reference evaluates the distance in float32
+// (create's float32 arrays) and that float32 value IS the answer; float
+// d < double r2 <=> d <= t0_max, the largest float below r2.  Later it uses
+// float64: the float32 distance of the same inputs is within ~3e-7 relative
+// (well inside the 1e-4 guard, which also covers float64 state rounded to
+// float32); a distance inside the guard band is flagged ambiguous and the
+// caller redoes its tests in float64 (a rare, whole-bullet slow path).
 struct Guard {
-    float lo, hi;
-    __device__ explicit Guard(double r2) : lo(float(r2 * (1.0 - 1e-4))), hi(float(r2 * (1.0 + 1e-4))) {}
+    float lo, hi, t0_max;
+    double r2;
+    __device__ explicit Guard(double r2_) : r2(r2_) {
+        lo = float(r2 * (1.0 - 1e-4));
+        hi = float(r2 * (1.0 + 1e-4));
+        float f = float(r2);                       // round to nearest (r2 > 0)
+        if (double(f) >= r2) f = __int_as_float(__float_as_int(f) - 1);
+        t0_max = f;
+    }
 };
+
+__device__ __forceinline__ bool closer32(float ax, float ay, float bx, float by, const Guard &g, bool t0,
+                                         bool &amb) {
+    const float dx = ax - bx;
+    const float dy = ay - by;
+    const float d2 = dx * dx + dy * dy;
+    amb = amb || (!t0 && d2 >= g.lo && d2 <= g.hi);
+    return t0 ? d2 <= g.t0_max : d2 < g.lo;
+}
 
 // Planet-on-planet gravity (core.py:291) for every planet i < np, in the
 // reference's summation order (j = 0..np-1, self term +0.0 included).  The
@@ -482,15 +488,25 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
         for (int u = 0; u < BCHUNK; ++u) {
             if (base + u < nb) {
                 const double x = double(cur[u].x), y = double(cur[u].y);
-                bool bh = false;
+                const float xf = float(cur[u].x), yf = float(cur[u].y);
+                bool bh = false, amb = false, hs[S];
 #pragma unroll
                 for (int j = 0; j < PMAX; ++j)
-                    if (j < np) bh = bh || closer(x, y, px[j], py[j], p.r2_p0, gp.lo, gp.hi, t0);
+                    if (j < np) bh = bh || closer32(xf, yf, float(px[j]), float(py[j]), gp, t0, amb);
+#pragma unroll
+                for (int s = 0; s < S; ++s) hs[s] = closer32(xf, yf, float(sx[s]), float(sy[s]), gs, t0, amb);
+                if (amb) {   // within 1e-4 of a threshold: the exact float64 tests
+                    bh = false;
+#pragma unroll
+                    for (int j = 0; j < PMAX; ++j)
+                        if (j < np) bh = bh || dist2<double>(x, y, px[j], py[j]) < p.r2_p0;
+#pragma unroll
+                    for (int s = 0; s < S; ++s) hs[s] = dist2<double>(x, y, sx[s], sy[s]) < p.r2_s0;
+                }
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
-                    const bool hs = closer(x, y, sx[s], sy[s], p.r2_s0, gs.lo, gs.hi, t0);
-                    bh = bh || hs;
-                    hit[s] = hit[s] || hs;
+                    bh = bh || hs[s];
+                    hit[s] = hit[s] || hs[s];
                 }
                 if (!bh) {
                     const C ndx = C(cur[u].z) + C(0), ndy = C(cur[u].w) + C(0);
@@ -649,19 +665,31 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         bool hit[S];
         {
             const Guard gsp(p.r2_sp), gss(p.r2_ss);
+            bool amb = false;
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 bool hs = false;
 #pragma unroll
                 for (int j = 0; j < PMAX; ++j)
-                    if (j < np) hs = hs || closer(sx[s], sy[s], px[j], py[j], p.r2_sp, gsp.lo, gsp.hi, t0);
+                    if (j < np)
+                        hs = hs || closer32(float(sx[s]), float(sy[s]), float(px[j]), float(py[j]), gsp, t0, amb);
                 hit[s] = hs;
             }
-            if (S == 2) {
-                const bool hh = closer(sx[0], sy[0], sx[S - 1], sy[S - 1], p.r2_ss, gss.lo, gss.hi, t0);
-                hit[0] = hit[0] || hh;
-                hit[S - 1] = hit[S - 1] || hh;
+            bool hh = false;
+            if (S == 2) hh = closer32(float(sx[0]), float(sy[0]), float(sx[S - 1]), float(sy[S - 1]), gss, t0, amb);
+            if (amb) {   // rare: the exact float64 tests
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    bool hs = false;
+#pragma unroll
+                    for (int j = 0; j < PMAX; ++j)
+                        if (j < np) hs = hs || dist2<double>(sx[s], sy[s], px[j], py[j]) < p.r2_sp;
+                    hit[s] = hs;
+                }
+                if (S == 2) hh = dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]) < p.r2_ss;
             }
+            hit[0] = hit[0] || hh;
+            hit[S - 1] = hit[S - 1] || hh;
         }
 
         STAMP(3);

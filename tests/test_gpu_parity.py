@@ -255,3 +255,54 @@ def test_full_size_determinism_and_shard_invariance():
     assert int(nb.max()) <= 32 and int(a.nplanets.min()) >= 1 and int(a.nplanets.max()) <= 4
     st = a.stat_dict()
     assert st['resets'] == st['collisions'] + st['timeouts'] > 0
+
+
+@pytest.mark.parametrize('tick', [0, 7])
+def test_near_threshold_collisions_exact(tick):
+    """Bodies placed within +-2e-4 (relative) of every collision threshold
+    (ship-ship, ship-planet, ship-bullet, bullet-planet), at tick 0 (float32
+    distances) and later (float64): hit flags, rewards and bullet survival
+    equal the oracle's exactly -- the kernel's float32 prefilter + guard band
+    must never decide a case the exact arithmetic decides differently."""
+    cfg = CFG['default']
+    P = batched.make_params(cfg)
+    n, bcap = 4096, 8
+    rng = np.random.RandomState(11 + tick)
+    B = batched.Batch.zeros(n, 2, 4, bcap)
+    B.tick[:] = tick
+    B.nplanets[:] = rng.randint(1, 5, n)
+    B.planets[..., 0:2] = rng.uniform(-0.6, 0.6, (n, 4, 2))
+    B.planets[..., 2:4] = rng.uniform(-0.1, 0.1, (n, 4, 2))
+    B.ships[..., 0:2] = rng.uniform(-0.9, 0.9, (n, 2, 2))
+    B.ships[..., 2:4] = rng.uniform(-0.2, 0.2, (n, 2, 2))
+    B.ships_b[:] = rng.uniform(-7, 7, (n, 2))
+
+    def around(c, r2):
+        ang = rng.uniform(0, 2 * np.pi, c.shape[:-1])
+        rad = np.sqrt(r2) * (1 + rng.uniform(-2e-4, 2e-4, c.shape[:-1]))
+        return c + np.stack([np.cos(ang), np.sin(ang)], -1) * rad[..., None]
+    kind = rng.randint(0, 3, n)
+    # ship 0 near planet 0 / near ship 1 / free
+    B.ships[kind == 0, 0, 0:2] = around(B.planets[kind == 0, 0, 0:2], P.r2_sp)
+    B.ships[kind == 1, 0, 0:2] = around(B.ships[kind == 1, 1, 0:2], P.r2_ss)
+    nb = rng.randint(0, bcap + 1, n)
+    B.nbullets[:] = nb
+    for k in range(bcap):
+        tgt = rng.randint(0, 2, n)
+        c = np.where(tgt[:, None] == 0, B.planets[:, 0, 0:2], B.ships[:, 1, 0:2])
+        r2 = np.where(tgt == 0, P.r2_p0, P.r2_s0)
+        B.bullets[:, k, 0:2] = around(c, r2)
+        B.bullets[:, k, 2:4] = rng.uniform(-1.5, 1.5, (n, 2))
+    for f in ('ships', 'ships_b', 'planets', 'bullets'):
+        a = getattr(B, f)
+        a[:] = a.astype(np.float32).astype(np.float64)
+    env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, p_pad=4)
+    env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
+    ctl = rng.randint(0, 6, size=(n, 2)).astype(np.int8)
+    want, wrew, wdone = batched.step(B, ctl, P, store='f32')
+    _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+    done = done.cpu().numpy()
+    assert (done == wdone).all()
+    assert np.array_equal(rew.cpu().numpy(), wrew)
+    _assert_same('near-threshold tick=%d' % tick, _host_batch(env), want, wdone == 0, rounding=True)
+    assert 0.05 < (wdone == 1).mean() < 0.95   # both outcomes well represented
