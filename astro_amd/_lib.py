@@ -9,11 +9,12 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'reserved')
 NSTATS = 8
+KERNELS = {'auto': 0, 'lane': 1, 'quad': 2}
 
 
 class AstroParams(ctypes.Structure):
@@ -41,6 +42,8 @@ class AstroParams(ctypes.Structure):
         ('b_cap', ctypes.c_int32),
         ('timeout_tick', ctypes.c_int32),
         ('fire_bits', ctypes.c_void_p),
+        ('kernel', ctypes.c_int32),
+        ('reserved', ctypes.c_int32),
     ]
 
 

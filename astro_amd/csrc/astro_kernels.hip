@@ -113,22 +113,23 @@ __device__ __forceinline__ C max_floor(C d2) {
 template <typename C, int PMAX>
 __device__ __forceinline__ void field(const double (&px)[PMAX], const double (&py)[PMAX], int np,
                                       double x, double y, double gm, C &gx, C &gy) {
+    // every slot is evaluated (padded slots hold a copy of planet 0) and the
+    // sum selects: a per-planet branch costs more than the arithmetic when
+    // some lane of the wave has all PMAX planets anyway
     C ax = C(0), ay = C(0);
 #pragma unroll
     for (int j = 0; j < PMAX; ++j) {
-        if (j < np) {
-            const C rx = C(px[j]) - C(x);
-            const C ry = C(py[j]) - C(y);
-            const C d2 = rx * rx + ry * ry;
-            const C f = C(gm) / max_floor(d2);
-            const C tx = f * rx, ty = f * ry;
-            if (j == 0) {
-                ax = tx;
-                ay = ty;
-            } else {
-                ax = ax + tx;
-                ay = ay + ty;
-            }
+        const C rx = C(px[j]) - C(x);
+        const C ry = C(py[j]) - C(y);
+        const C d2 = rx * rx + ry * ry;
+        const C f = C(gm) / max_floor(d2);
+        const C tx = f * rx, ty = f * ry;
+        if (j == 0) {
+            ax = tx;
+            ay = ty;
+        } else {
+            ax = j < np ? ax + tx : ax;
+            ay = j < np ? ay + ty : ay;
         }
     }
     gx = ax;
@@ -165,12 +166,12 @@ struct Guard {
 };
 
 __device__ __forceinline__ bool closer32(float ax, float ay, float bx, float by, const Guard &g, bool t0,
-                                         bool &amb) {
+                                         bool valid, bool &amb) {
     const float dx = ax - bx;
     const float dy = ay - by;
     const float d2 = dx * dx + dy * dy;
-    amb = amb || (!t0 && d2 >= g.lo && d2 <= g.hi);
-    return t0 ? d2 <= g.t0_max : d2 < g.lo;
+    amb |= valid & !t0 & (d2 >= g.lo) & (d2 <= g.hi);
+    return valid & (t0 ? d2 <= g.t0_max : d2 < g.lo);
 }
 
 // Planet-on-planet gravity (core.py:291) for every planet i < np, in the
@@ -194,11 +195,9 @@ __device__ __forceinline__ void planet_field(const double (&px)[PMAX], const dou
     for (int i = 0; i < PMAX; ++i) {
 #pragma unroll
         for (int j = i + 1; j < PMAX; ++j) {
-            if (j < np) {
-                const C rx = C(px[j]) - C(px[i]);
-                const C ry = C(py[j]) - C(py[i]);
-                f[i][j] = C(gm) / max_floor(rx * rx + ry * ry);
-            }
+            const C rx = C(px[j]) - C(px[i]);
+            const C ry = C(py[j]) - C(py[i]);
+            f[i][j] = C(gm) / max_floor(rx * rx + ry * ry);
         }
     }
 #pragma unroll
@@ -206,25 +205,23 @@ __device__ __forceinline__ void planet_field(const double (&px)[PMAX], const dou
         C ax = C(0), ay = C(0);
 #pragma unroll
         for (int j = 0; j < PMAX; ++j) {
-            if (j < np) {
-                C tx, ty;
-                if (j == i) {
-                    tx = C(0);
-                    ty = C(0);
-                } else {
-                    const C rx = C(px[j]) - C(px[i]);
-                    const C ry = C(py[j]) - C(py[i]);
-                    const C fij = j > i ? f[i][j] : f[j][i];
-                    tx = fij * rx;
-                    ty = fij * ry;
-                }
-                if (j == 0) {
-                    ax = tx;
-                    ay = ty;
-                } else {
-                    ax = ax + tx;
-                    ay = ay + ty;
-                }
+            C tx, ty;
+            if (j == i) {
+                tx = C(0);
+                ty = C(0);
+            } else {
+                const C rx = C(px[j]) - C(px[i]);
+                const C ry = C(py[j]) - C(py[i]);
+                const C fij = j > i ? f[i][j] : f[j][i];
+                tx = fij * rx;
+                ty = fij * ry;
+            }
+            if (j == 0) {
+                ax = tx;
+                ay = ty;
+            } else {
+                ax = j < np ? ax + tx : ax;
+                ay = j < np ? ay + ty : ay;
             }
         }
         gx[i] = ax;
@@ -473,6 +470,17 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
     using V = typename Store<T>::V;
     const C dt = C(p.dt);
     const Guard gp(p.r2_p0), gs(p.r2_s0);
+    float pxf[PMAX], pyf[PMAX], sxf[S], syf[S];
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) {
+        pxf[j] = float(px[j]);
+        pyf[j] = float(py[j]);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        sxf[s] = float(sx[s]);
+        syf[s] = float(sy[s]);
+    }
     for (int base = 0; base < nb; base += BCHUNK) {
         // prefetch the next chunk before working on this one (slots read
         // ahead are never below the write cursor: w <= slot being read)
@@ -486,48 +494,52 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
         }
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) {
-            if (base + u < nb) {
-                const double x = double(cur[u].x), y = double(cur[u].y);
-                const float xf = float(cur[u].x), yf = float(cur[u].y);
-                bool bh = false, amb = false, hs[S];
+            // branch-free: every slot of the chunk is evaluated (slots past nb
+            // hold a copy of slot 0); only the store and the rare exact
+            // recheck are conditional
+            const bool valid = base + u < nb;
+            const double x = double(cur[u].x), y = double(cur[u].y);
+            const float xf = float(cur[u].x), yf = float(cur[u].y);
+            bool bh = false, amb = false, hs[S];
 #pragma unroll
-                for (int j = 0; j < PMAX; ++j)
-                    if (j < np) bh = bh || closer32(xf, yf, float(px[j]), float(py[j]), gp, t0, amb);
+            for (int j = 0; j < PMAX; ++j) bh |= closer32(xf, yf, pxf[j], pyf[j], gp, t0, valid & (j < np), amb);
 #pragma unroll
-                for (int s = 0; s < S; ++s) hs[s] = closer32(xf, yf, float(sx[s]), float(sy[s]), gs, t0, amb);
-                if (amb) {   // within 1e-4 of a threshold: the exact float64 tests
-                    bh = false;
+            for (int s = 0; s < S; ++s) hs[s] = closer32(xf, yf, sxf[s], syf[s], gs, t0, valid, amb);
+#ifdef ASTRO_COLLIDE_F64
+            amb = valid;   // variant: always the exact float64 tests
+#endif
+            if (__any(amb)) {   // some lane within 1e-4 of a threshold: exact float64
+                bool bh64 = false, hs64[S];
 #pragma unroll
-                    for (int j = 0; j < PMAX; ++j)
-                        if (j < np) bh = bh || dist2<double>(x, y, px[j], py[j]) < p.r2_p0;
+                for (int j = 0; j < PMAX; ++j) bh64 |= (j < np) & (dist2<double>(x, y, px[j], py[j]) < p.r2_p0);
 #pragma unroll
-                    for (int s = 0; s < S; ++s) hs[s] = dist2<double>(x, y, sx[s], sy[s]) < p.r2_s0;
-                }
+                for (int s = 0; s < S; ++s) hs64[s] = dist2<double>(x, y, sx[s], sy[s]) < p.r2_s0;
+                bh = amb ? bh64 : bh;
 #pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    bh = bh || hs[s];
-                    hit[s] = hit[s] || hs[s];
-                }
-                if (!bh) {
-                    const C ndx = C(cur[u].z) + C(0), ndy = C(cur[u].w) + C(0);
-                    const C nx = C(x) + dt * ndx, ny = C(y) + dt * ndy;
-                    const bool keep = (C(-1) <= nx && nx <= C(1)) || (C(-1) <= ny && ny <= C(1));
-                    const bool fits = w < p.b_cap;
-                    if (keep && fits) {
-                        V v;
-                        v.x = T(nx);
-                        v.y = T(ny);
-                        v.z = T(ndx);
-                        v.w = T(ndy);
-                        bullets[size_t(w) * NN + i] = v;
-                    }
-                    // counters as arithmetic: a conditional ++ of one of two
-                    // locals is folded into a store through a selected
-                    // pointer, which sends both to scratch memory
-                    w += int(keep && fits);
-                    dropped += int(keep && !fits);
-                }
+                for (int s = 0; s < S; ++s) hs[s] = amb ? hs64[s] : hs[s];
             }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                bh |= hs[s];
+                hit[s] |= valid & hs[s];
+            }
+            const C ndx = C(cur[u].z) + C(0), ndy = C(cur[u].w) + C(0);
+            const C nx = C(x) + dt * ndx, ny = C(y) + dt * ndy;
+            const bool keep = valid & !bh & ((C(-1) <= nx && nx <= C(1)) || (C(-1) <= ny && ny <= C(1)));
+            const bool fits = w < p.b_cap;
+            if (keep & fits) {
+                V v;
+                v.x = T(nx);
+                v.y = T(ny);
+                v.z = T(ndx);
+                v.w = T(ndy);
+                bullets[size_t(w) * NN + i] = v;
+            }
+            // counters as arithmetic: a conditional ++ of one of two locals
+            // is folded into a store through a selected pointer, which sends
+            // both to scratch memory
+            w += int(keep & fits);
+            dropped += int(keep & !fits);
         }
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) cur[u] = nxt[u];
@@ -569,8 +581,13 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                                                            int auto_reset) {
     using V = typename Store<T>::V;
     const int N = st.n_env;
+#ifdef ASTRO_ENVS_PER_WAVE   // occupancy experiment: fewer envs per wave
+    const int i = blockIdx.x * ASTRO_ENVS_PER_WAVE + int(threadIdx.x);
+    const bool active = i < N && int(threadIdx.x) < ASTRO_ENVS_PER_WAVE;
+#else
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool active = i < N;
+#endif
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
     bool f_reset = false, f_coll = false, f_tout = false;
 #ifdef ASTRO_STAMPS
@@ -671,22 +688,25 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                 bool hs = false;
 #pragma unroll
                 for (int j = 0; j < PMAX; ++j)
-                    if (j < np)
-                        hs = hs || closer32(float(sx[s]), float(sy[s]), float(px[j]), float(py[j]), gsp, t0, amb);
+                    hs |= closer32(float(sx[s]), float(sy[s]), float(px[j]), float(py[j]), gsp, t0, j < np, amb);
                 hit[s] = hs;
             }
             bool hh = false;
-            if (S == 2) hh = closer32(float(sx[0]), float(sy[0]), float(sx[S - 1]), float(sy[S - 1]), gss, t0, amb);
-            if (amb) {   // rare: the exact float64 tests
+            if (S == 2)
+                hh = closer32(float(sx[0]), float(sy[0]), float(sx[S - 1]), float(sy[S - 1]), gss, t0, true, amb);
+#ifdef ASTRO_COLLIDE_F64
+            amb = !t0;
+#endif
+            if (__any(amb)) {   // rare: the exact float64 tests, for the ambiguous lanes
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     bool hs = false;
 #pragma unroll
                     for (int j = 0; j < PMAX; ++j)
-                        if (j < np) hs = hs || dist2<double>(sx[s], sy[s], px[j], py[j]) < p.r2_sp;
-                    hit[s] = hs;
+                        hs |= (j < np) & (dist2<double>(sx[s], sy[s], px[j], py[j]) < p.r2_sp);
+                    hit[s] = amb ? hs : hit[s];
                 }
-                if (S == 2) hh = dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]) < p.r2_ss;
+                if (S == 2) hh = amb ? (dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]) < p.r2_ss) : hh;
             }
             hit[0] = hit[0] || hh;
             hit[S - 1] = hit[S - 1] || hh;
@@ -857,6 +877,418 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
     }
 }
 
+// ---------------------------------------------------------------------------
+// The quad kernel: FOUR lanes per env (16 envs per wave).
+//
+// At 65,536 envs a lane-per-env launch is 1,024 waves = one per SIMD, and one
+// wave alone issues a VALU op at best every 4 cycles with nothing to hide
+// its waits (measured: 3.1k VALU ops + 17k cycles of waits per wave).  Here
+// the same envs make 4,096 waves (4 per SIMD) and each lane does a quarter of
+// its env: lane q owns planet slots q, q+4, .. and bullet slots q, q+4, ..;
+// lanes 0..S-1 own the ships.  Positions are broadcast inside the quad with
+// DPP quad_perm (no LDS, no memory), hit flags are OR-ed and surviving
+// bullets compacted in order with one ballot per round.  Every float64 sum
+// keeps the reference's sequential order, so results are bit-identical to
+// the lane-per-env kernel.
+
+template <int J>
+__device__ __forceinline__ int quad_bcast_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xf, 0xf, false);   // quad_perm(J,J,J,J)
+}
+template <int J>
+__device__ __forceinline__ float quad_bcast(float v) {
+    return __int_as_float(quad_bcast_i<J>(__float_as_int(v)));
+}
+template <int J>
+__device__ __forceinline__ double quad_bcast(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = quad_bcast_i<J>(int(b & 0xffffffffll));
+    const int hi = quad_bcast_i<J>(int(b >> 32));
+    return __longlong_as_double((long long)(uint32_t(lo)) | ((long long)hi << 32));
+}
+
+// broadcast slot m of lane J of the quad into out[4*m + J]
+template <typename T, int J, int PPL>
+__device__ __forceinline__ void bcast_slots(const T (&mine)[PPL], double (&out)[4 * PPL]) {
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) out[4 * m + J] = double(quad_bcast<J>(mine[m]));
+}
+
+// OR of a per-lane flag over the lane's quad (all quad lanes must be active)
+__device__ __forceinline__ bool quad_any(bool f, int lane) {
+    return ((__ballot(f) >> (lane & ~3)) & 0xfull) != 0;
+}
+
+constexpr int QB = 4;   // bullet rounds per prefetched chunk (16 bullets per quad)
+
+template <typename T, int S, int PMAX>
+__global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st,
+                                                                const int8_t *__restrict__ control,
+                                                                float *__restrict__ reward,
+                                                                uint8_t *__restrict__ done_out,
+                                                                unsigned long long *stats, int auto_reset) {
+    using V = typename Store<T>::V;
+    constexpr int PPL = PMAX / 4;   // planet slots per lane
+    const int N = st.n_env;
+    const int lane = threadIdx.x & 63;
+    const int q = lane & 3;
+    const int i = (blockIdx.x * BLOCK + threadIdx.x) >> 2;
+    const bool active = i < N;   // uniform over the quad
+    uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
+    bool f_reset = false, f_coll = false, f_tout = false;
+
+    if (active) {
+        const size_t NN = size_t(N);
+        V *ships = reinterpret_cast<V *>(st.ships);
+        T *ships_b = reinterpret_cast<T *>(st.ships_b);
+        V *planets = reinterpret_cast<V *>(st.planets);
+        V *bullets = reinterpret_cast<V *>(st.bullets);
+
+        // ---- loads: header (every lane), own ship (lanes < S)
+        const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+        const int sq = q < S ? q : 0;
+        const V sv = ships[size_t(sq) * NN + i];
+        const T sbv = ships_b[size_t(sq) * NN + i];
+        const int ctl = int(control[size_t(i) * S + sq]);
+        const int tick = int(uint32_t(h.x) & TICK_MASK);
+        const uint32_t pend_j = uint32_t(h.x) >> TICK_BITS;
+        const uint32_t pend_v = uint32_t(h.z);
+        int np = h.y & 0xff;
+        int flags = (h.y >> 8) & 0xff;
+        const int nb = int(uint32_t(h.y) >> 16);
+        np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+        const bool live = tick < p.timeout_tick;
+        const bool t0 = tick == 0;
+
+        // ---- own planet slots (padded ones re-read slot 0), first bullet chunk
+        V pv[PPL];
+        T mpx[PPL], mpy[PPL];
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + 4 * m;
+            pv[m] = planets[size_t(j < np ? j : 0) * NN + i];
+            mpx[m] = pv[m].x;
+            mpy[m] = pv[m].y;
+        }
+        const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
+        const int rounds = (nb + 3) >> 2;
+        V cur[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+            const int k = q + 4 * u;
+            cur[u] = bullets[size_t(k < nb ? k : 0) * NN + i];
+        }
+        n_pl = q == 0 ? uint32_t(np) : 0u;
+
+        // ---- quad broadcasts (uniform control flow): all planets, both ships
+        double px[PMAX], py[PMAX], sx[S], sy[S];
+        bcast_slots<T, 0, PPL>(mpx, px);
+        bcast_slots<T, 1, PPL>(mpx, px);
+        bcast_slots<T, 2, PPL>(mpx, px);
+        bcast_slots<T, 3, PPL>(mpx, px);
+        bcast_slots<T, 0, PPL>(mpy, py);
+        bcast_slots<T, 1, PPL>(mpy, py);
+        bcast_slots<T, 2, PPL>(mpy, py);
+        bcast_slots<T, 3, PPL>(mpy, py);
+        sx[0] = double(quad_bcast<0>(sv.x));
+        sy[0] = double(quad_bcast<0>(sv.y));
+        if (S == 2) {
+            sx[S - 1] = double(quad_bcast<S - 1>(sv.x));
+            sy[S - 1] = double(quad_bcast<S - 1>(sv.y));
+        }
+
+        // ---- own ship (lanes < S): direction, thrust + gravity (core.py:234-239)
+        const double mx = double(sv.x), my = double(sv.y), mdx = double(sv.z), mdy = double(sv.w);
+        const double mb = double(sbv);
+        float ds, dc;
+        np_sincosf(float(mb), ds, dc);
+        double ax = 0.0, ay = 0.0;
+        if (q < S) {
+            double gx, gy;
+            if (t0) {
+                float fx, fy;
+                field<float, PMAX>(px, py, np, mx, my, p.gm, fx, fy);
+                gx = double(fx);
+                gy = double(fy);
+            } else {
+                field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy);
+            }
+            const double thr = p.thrust * double(ctl & 1);
+            ax = thr * double(ds) + gx;
+            ay = thr * double(dc) + gy;
+        }
+
+        // ---- collisions (core.py:241-253): lane q tests its planets and its
+        //      bullets against every ship; quad-OR afterwards
+        const Guard gsp(p.r2_sp), gss(p.r2_ss), gp(p.r2_p0), gs(p.r2_s0);
+        float pxf[PMAX], pyf[PMAX], sxf[S], syf[S];
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+            pxf[j] = float(px[j]);
+            pyf[j] = float(py[j]);
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            sxf[s] = float(sx[s]);
+            syf[s] = float(sy[s]);
+        }
+        bool hsp[S];
+        {
+            bool amb = false;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                bool hs = false;
+#pragma unroll
+                for (int m = 0; m < PPL; ++m) {
+                    const int j = q + 4 * m;
+                    hs |= closer32(sxf[s], syf[s], float(mpx[m]), float(mpy[m]), gsp, t0, j < np, amb);
+                }
+                hsp[s] = hs;
+            }
+            bool hh = false;
+            if (S == 2 && q == 0) hh = closer32(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, t0, true, amb);
+            if (__any(amb)) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    bool hs = false;
+#pragma unroll
+                    for (int m = 0; m < PPL; ++m) {
+                        const int j = q + 4 * m;
+                        hs |= (j < np) & (dist2<double>(sx[s], sy[s], double(mpx[m]), double(mpy[m])) < p.r2_sp);
+                    }
+                    hsp[s] = amb ? hs : hsp[s];
+                }
+                if (S == 2 && q == 0) hh = amb ? (dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]) < p.r2_ss) : hh;
+            }
+#pragma unroll
+            for (int s = 0; s < S; ++s) hsp[s] = hsp[s] || hh;
+        }
+
+        // ---- bullets: round r handles slots 4r..4r+3 of the quad; survivors
+        //      compacted in slot order with one ballot per round
+        int wr = 0;   // survivors so far (same in the 4 lanes), may exceed b_cap
+        const double dt = p.dt;
+        bool hsb[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) hsb[s] = false;
+        const uint64_t below = (1ull << q) - 1;
+        for (int r0 = 0; r0 < rounds; r0 += QB) {
+            V nxt[QB];
+            if (r0 + QB < rounds) {
+#pragma unroll
+                for (int u = 0; u < QB; ++u) {
+                    const int k = q + 4 * (r0 + QB + u);
+                    nxt[u] = bullets[size_t(k < nb ? k : 0) * NN + i];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < QB; ++u) {
+                if (r0 + u < rounds) {   // uniform over the quad
+                    const bool valid = q + 4 * (r0 + u) < nb;
+                    const float xf = float(cur[u].x), yf = float(cur[u].y);
+                    const double x = double(cur[u].x), y = double(cur[u].y);
+                    bool bh = false, amb = false, hs[S];
+#pragma unroll
+                    for (int j = 0; j < PMAX; ++j) bh |= closer32(xf, yf, pxf[j], pyf[j], gp, t0, valid & (j < np), amb);
+#pragma unroll
+                    for (int s = 0; s < S; ++s) hs[s] = closer32(xf, yf, sxf[s], syf[s], gs, t0, valid, amb);
+                    if (__any(amb)) {
+                        bool bh64 = false, hs64[S];
+#pragma unroll
+                        for (int j = 0; j < PMAX; ++j) bh64 |= (j < np) & (dist2<double>(x, y, px[j], py[j]) < p.r2_p0);
+#pragma unroll
+                        for (int s = 0; s < S; ++s) hs64[s] = dist2<double>(x, y, sx[s], sy[s]) < p.r2_s0;
+                        bh = amb ? bh64 : bh;
+#pragma unroll
+                        for (int s = 0; s < S; ++s) hs[s] = amb ? hs64[s] : hs[s];
+                    }
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        bh |= hs[s];
+                        hsb[s] |= valid & hs[s];
+                    }
+                    bool keep;
+                    V out;
+                    if (t0) {
+                        const float dtf = float(p.dt);
+                        const float ndx = float(cur[u].z) + 0.0f, ndy = float(cur[u].w) + 0.0f;
+                        const float nx = float(x) + dtf * ndx, ny = float(y) + dtf * ndy;
+                        keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
+                        out.x = T(nx);
+                        out.y = T(ny);
+                        out.z = T(ndx);
+                        out.w = T(ndy);
+                    } else {
+                        const double ndx = double(cur[u].z) + 0.0, ndy = double(cur[u].w) + 0.0;
+                        const double nx = x + dt * ndx, ny = y + dt * ndy;
+                        keep = (-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0);
+                        out.x = T(nx);
+                        out.y = T(ny);
+                        out.z = T(ndx);
+                        out.w = T(ndy);
+                    }
+                    keep = keep & valid & !bh;
+                    const uint64_t nib = (__ballot(keep) >> (lane & ~3)) & 0xfull;
+                    const int pos = wr + __popcll(nib & below);
+                    if (keep && pos < p.b_cap) bullets[size_t(pos) * NN + i] = out;
+                    wr += __popcll(nib);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < QB; ++u) cur[u] = nxt[u];
+        }
+        n_bin = q == 0 ? uint32_t(nb) : 0u;
+
+        bool hit[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) hit[s] = quad_any(hsp[s] || hsb[s], lane);
+        const bool collided = S == 2 ? (hit[0] || hit[S - 1]) : hit[0];
+        const bool timeout = !collided && !live;
+        const uint8_t done = collided ? 1 : (timeout ? 2 : 0);
+        if (q < S) {   // rewards (core.py:253-260): lane s writes ship s's
+            const bool mh = q == 0 ? hit[0] : hit[S - 1];
+            reward[size_t(i) * S + q] = collided ? (mh ? -1.0f : 1.0f) : (timeout ? p.timeout_reward : 0.0f);
+        }
+        if (q == 0) done_out[i] = done;
+
+        if (!done) {   // uniform over the quad
+            // ---- fire: ship s's bullet appended after the survivors, in ship order
+            if ((fire_word >> (tick & 31)) & 1u) {
+                bool keep = false;
+                V out;
+                if (q < S) {
+                    const float os = p.spawn_off * ds, oc = p.spawn_off * dc;
+                    const float vs = p.bullet_speed * ds, vc = p.bullet_speed * dc;
+                    if (t0) {
+                        const float dtf = float(p.dt);
+                        const float bx = float(mx) + os, by = float(my) + oc;
+                        const float bdx = (float(mdx) + vs) + 0.0f, bdy = (float(mdy) + vc) + 0.0f;
+                        const float nx = bx + dtf * bdx, ny = by + dtf * bdy;
+                        keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
+                        out.x = T(nx);
+                        out.y = T(ny);
+                        out.z = T(bdx);
+                        out.w = T(bdy);
+                    } else {
+                        const double bx = mx + double(os), by = my + double(oc);
+                        const double bdx = (mdx + double(vs)) + 0.0, bdy = (mdy + double(vc)) + 0.0;
+                        const double nx = bx + p.dt * bdx, ny = by + p.dt * bdy;
+                        keep = (-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0);
+                        out.x = T(nx);
+                        out.y = T(ny);
+                        out.z = T(bdx);
+                        out.w = T(bdy);
+                    }
+                }
+                const uint64_t nib = (__ballot(keep) >> (lane & ~3)) & 0xfull;
+                const int pos = wr + __popcll(nib & below);
+                if (keep && pos < p.b_cap) bullets[size_t(pos) * NN + i] = out;
+                wr += __popcll(nib);
+            }
+            const int w = wr < p.b_cap ? wr : p.b_cap;
+            const int dropped = wr - w;
+
+            // ---- own ship: semi-implicit Euler + wrap (core.py:283-288)
+            if (q < S) {
+                const double ndx = mdx + ax * p.dt;
+                const double ndy = mdy + ay * p.dt;
+                V v;
+                v.x = T(wrap_unit<double>(mx + p.dt * ndx));
+                v.y = T(wrap_unit<double>(my + p.dt * ndy));
+                v.z = T(ndx);
+                v.w = T(ndy);
+                ships[size_t(q) * NN + i] = v;
+                ships_b[size_t(q) * NN + i] = T(mb + p.db * double((ctl >> 1) - 1));
+            }
+
+            // ---- own planets: gravity of all planets incl. self, in order
+            //      (core.py:289-294); float32 at tick 0 / for a lone planet
+            const float dtf = float(p.dt);
+#pragma unroll
+            for (int m = 0; m < PPL; ++m) {
+                const int j = q + 4 * m;
+                if (j < np) {
+                    const double pxj = double(mpx[m]), pyj = double(mpy[m]);
+                    const double pdx = double(pv[m].z), pdy = double(pv[m].w);
+                    V v;
+                    if (np == 1) {
+                        float gx, gy;
+                        field<float, PMAX>(px, py, 1, pxj, pyj, p.gm, gx, gy);
+                        const float ndx = float(pdx) + gx * dtf, ndy = float(pdy) + gy * dtf;
+                        v.x = T(wrap_unit<float>(float(pxj) + dtf * ndx));
+                        v.y = T(wrap_unit<float>(float(pyj) + dtf * ndy));
+                        v.z = T(ndx);
+                        v.w = T(ndy);
+                    } else {
+                        double ndx, ndy;
+                        if (t0) {
+                            float gx, gy;
+                            field<float, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
+                            ndx = pdx + double(gx * dtf);
+                            ndy = pdy + double(gy * dtf);
+                        } else {
+                            double gx, gy;
+                            field<double, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
+                            ndx = pdx + gx * p.dt;
+                            ndy = pdy + gy * p.dt;
+                        }
+                        v.x = T(wrap_unit<double>(pxj + p.dt * ndx));
+                        v.y = T(wrap_unit<double>(pyj + p.dt * ndy));
+                        v.z = T(ndx);
+                        v.w = T(ndy);
+                    }
+                    planets[size_t(j) * NN + i] = v;
+                }
+            }
+
+            if (q == 0) {
+                const int fl = flags | (dropped ? 1 : 0);
+                uint32_t v = pend_v, j = pend_j;
+#pragma unroll
+                for (uint32_t k = 0; k < MT_STEPS_PER_TICK; ++k) {
+                    if (j < MT_PROLOGUE) {
+                        ++j;
+                        v = mt_key_next(v, j);
+                    }
+                }
+                reinterpret_cast<int4 *>(st.hdr)[i] =
+                    make_int4(int(uint32_t(tick + 1) | (j << TICK_BITS)), np | (fl << 8) | (w << 16), int(v), h.w);
+                n_bout = uint32_t(w);
+                n_drop = uint32_t(dropped);
+            }
+        } else if (q == 0) {
+            f_coll = collided;
+            f_tout = timeout;
+            if (auto_reset) {
+                restart_from_stream<T, S, PMAX>(p, st, i, pend_v, pend_j, uint32_t(h.w));
+                f_reset = true;
+            }
+        }
+    }
+
+    if (stats) {   // one private row per wave (16 envs)
+        const uint64_t m_reset = __ballot(f_reset), m_coll = __ballot(f_coll), m_tout = __ballot(f_tout);
+        const bool packed = p.b_cap <= 1023;
+        const uint32_t a = wave_sum32(packed ? (n_bin | (n_bout << 16)) : n_bin);
+        const uint32_t b = wave_sum32(packed ? (n_pl | (n_drop << 16)) : n_bout);
+        const uint32_t c = packed ? 0u : wave_sum32(n_pl | (n_drop << 16));
+        if (lane == 0) {
+            unsigned long long *slot = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * ASTRO_NSTATS;
+            const uint64_t bin = packed ? (a & 0xffff) : a;
+            const uint64_t bout = packed ? (a >> 16) : b;
+            const uint64_t pl = packed ? (b & 0xffff) : (c & 0xffff);
+            const uint64_t drop = packed ? (b >> 16) : (c >> 16);
+            if (bin) atomicAdd(slot + ASTRO_STAT_BULLETS_IN, (unsigned long long)bin);
+            if (bout) atomicAdd(slot + ASTRO_STAT_BULLETS_OUT, (unsigned long long)bout);
+            if (m_reset) atomicAdd(slot + ASTRO_STAT_RESETS, (unsigned long long)__popcll(m_reset));
+            if (m_coll) atomicAdd(slot + ASTRO_STAT_COLLISIONS, (unsigned long long)__popcll(m_coll));
+            if (m_tout) atomicAdd(slot + ASTRO_STAT_TIMEOUTS, (unsigned long long)__popcll(m_tout));
+            if (drop) atomicAdd(slot + ASTRO_STAT_OVERFLOWS, (unsigned long long)drop);
+            if (pl) atomicAdd(slot + ASTRO_STAT_PLANETS, (unsigned long long)pl);
+        }
+    }
+}
+
 template <typename T, int S, int PMAX>
 __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, AstroState st,
                                                             const uint32_t *__restrict__ seeds,
@@ -927,6 +1359,7 @@ int check_params(const AstroParams *p) {
     if (p->b_cap < 1 || p->b_cap > 65535) return fail(-15, "b_cap must be in [1, 65535]");
     if (p->timeout_tick < 0 || p->timeout_tick >= int(TICK_MASK)) return fail(-16, "timeout_tick out of [0, 2^22)");
     if (p->timeout_tick > 0 && !p->fire_bits) return fail(-17, "fire_bits is NULL");
+    if (p->kernel < 0 || p->kernel > 2) return fail(-18, "kernel must be 0 (auto), 1 (lane) or 2 (quad)");
     return 0;
 }
 
@@ -936,12 +1369,31 @@ int launched(const char *what) {
     return 0;
 }
 
+// kernel choice: the quad kernel fills the chip with 4 waves per SIMD where a
+// lane per env would leave it at <= 2 (fewer than 2 x 64 x 1024 envs); past
+// that the lane-per-env kernel has the occupancy and fewer instructions
+int pick_kernel(const AstroParams &p, int n_env) {
+    if (p.kernel == ASTRO_KERNEL_LANE || p.kernel == ASTRO_KERNEL_QUAD) return p.kernel;
+    return n_env <= ASTRO_QUAD_MAX_ENVS ? ASTRO_KERNEL_QUAD : ASTRO_KERNEL_LANE;
+}
+
 template <typename T, int S, int PM>
 int launch_step(const AstroParams &p, const AstroState &s, const int8_t *c, float *r, uint8_t *d,
                 uint64_t *stats, int ar, hipStream_t stream) {
+    unsigned long long *st = reinterpret_cast<unsigned long long *>(stats);
+    if (pick_kernel(p, s.n_env) == ASTRO_KERNEL_QUAD) {
+        const int grid = int((int64_t(s.n_env) * 4 + BLOCK - 1) / BLOCK);
+        hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, c, r, d,
+                           st, ar);
+        return launched("astro_step(quad)");
+    }
+#ifdef ASTRO_ENVS_PER_WAVE
+    const int grid = (s.n_env + ASTRO_ENVS_PER_WAVE - 1) / ASTRO_ENVS_PER_WAVE;
+    st = nullptr;
+#else
     const int grid = (s.n_env + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL((astro_step_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, c, r, d,
-                       reinterpret_cast<unsigned long long *>(stats), ar);
+#endif
+    hipLaunchKernelGGL((astro_step_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, c, r, d, st, ar);
     return launched("astro_step");
 }
 
@@ -1001,6 +1453,7 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
     if (auto_reset && !s->stream) return fail(-31, "auto_reset needs the stream array");
     if (p->nships == 2 && ((reinterpret_cast<uintptr_t>(control) & 1u) || (reinterpret_cast<uintptr_t>(reward) & 7u)))
         return fail(-32, "control must be 2-byte and reward 8-byte aligned");
+    if (int64_t(s->n_env) * 4 > int64_t(0x7fffffff)) return fail(-34, "n_env too large");
     if (stats && (reinterpret_cast<uintptr_t>(stats) & 7u)) return fail(-33, "stats must be 8-byte aligned");
     return dispatch<StepL>(*p, *s, control, reward, done, stats, int(auto_reset),
                            reinterpret_cast<hipStream_t>(stream));

@@ -51,10 +51,12 @@ class BatchedEnv:
     p_pad      -- planet slots per env (default: config.max_planets)
     dtype      -- torch.float32 (default) or torch.float64 state storage
     env_offset -- global id of env 0 (multi-GPU sharding)
+    kernel     -- 'auto', 'lane' (one lane per env) or 'quad' (four lanes
+                  per env); identical results, different speed
     """
 
     def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
-                 dtype=torch.float32, env_offset=0, auto_reset=True):
+                 dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto'):
         _schedule.check_config(config)
         if dtype not in (torch.float32, torch.float64):
             raise ValueError('dtype must be torch.float32 or torch.float64')
@@ -84,13 +86,13 @@ class BatchedEnv:
         self.stream = z(N, 4, dt=torch.int32)
         self.reward = z(N, S, dt=torch.float32)
         self.done = z(N, dt=torch.uint8)
-        self.stats = z(max(1, (N + 63) // 64), _lib.NSTATS, dt=torch.int64)
+        self.stats = z(max(1, (N + 15) // 16), _lib.NSTATS, dt=torch.int64)
         self.fire_bits = torch.from_numpy(self.schedule.fire_bits().view(np.int32)).to(dev)
 
         k = _schedule.kernel_constants(config)
         self.params = _lib.AstroParams(
             p_pad=self.p_pad, b_cap=self.b_cap, timeout_tick=self.schedule.timeout_tick,
-            fire_bits=self.fire_bits.data_ptr(), **k)
+            fire_bits=self.fire_bits.data_ptr(), kernel=_lib.KERNELS[kernel], **k)
         self.state = _lib.AstroState(
             ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),
             planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 2
+#define ASTRO_ABI_VERSION 3
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -62,7 +62,15 @@ typedef struct AstroParams {
     int32_t b_cap;         /* bullet slots per env, 1..65535 */
     int32_t timeout_tick;  /* first tick k with max_time <= t_k + dt */
     const uint32_t *fire_bits; /* device: bit k = fire on tick k, k < timeout_tick */
+    int32_t kernel;        /* ASTRO_KERNEL_AUTO / _LANE / _QUAD (results are identical) */
+    int32_t reserved;
 } AstroParams;
+
+/* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:
+ * four lanes per env (16 envs per wave), for batches too small to give each
+ * SIMD several waves.  AUTO picks QUAD for n_env <= ASTRO_QUAD_MAX_ENVS. */
+enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2 };
+#define ASTRO_QUAD_MAX_ENVS 131072
 
 /* Per-env state arrays (device pointers).  hdr packs
  *   hdr[4*i+0] = tick (steps since create, < 2^22) | chain progress j << 22
@@ -85,9 +93,9 @@ typedef struct AstroState {
 } AstroState;
 
 /* Statistics accumulated by astro_step when `stats` is non-NULL: uint64
- * [ceil(n_env / 64)][ASTRO_NSTATS], one private row per wave64 (env block
- * 64*w .. 64*w+63), added to and never cleared by the library.  Sum the rows
- * for totals.  (A private row per wave keeps the counters contention-free:
+ * [ceil(n_env / 16)][ASTRO_NSTATS], one private row per wave64 (a wave covers
+ * 64 envs in the LANE kernel, 16 in the QUAD kernel), added to and never
+ * cleared by the library.  Sum the rows for totals.  (A private row per wave keeps the counters contention-free:
  * every wave adding into one shared row serialises at the memory side.) */
 enum {
     ASTRO_STAT_BULLETS_IN = 0,  /* live bullets read */

@@ -19,10 +19,13 @@ pytestmark = pytest.mark.gpu
 CFG = gio.configs()
 
 
-def _env(cfg, n, dtype=torch.float64, b_cap=64, p_pad=8, auto_reset=False):
+KERNELS = ['lane', 'quad']
+
+
+def _env(cfg, n, dtype=torch.float64, b_cap=64, p_pad=8, auto_reset=False, kernel='auto'):
     from astro_amd import BatchedEnv
     return BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, dtype=dtype,
-                      auto_reset=auto_reset)
+                      auto_reset=auto_reset, kernel=kernel)
 
 
 def _host_batch(env):
@@ -87,16 +90,17 @@ def test_seed_streams_follow_generate_configs():
 
 # ------------------------------------------------- teacher-forced transitions
 
+@pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
 @pytest.mark.parametrize('fname', ['steps.npz', 'edge_steps.npz'])
-def test_step_teacher_forced_vs_reference(fname, dtype):
+def test_step_teacher_forced_vs_reference(fname, dtype, kernel):
     tr = gio.Transitions(fname)
     for name, idx in tr.groups():
         cfg = CFG[name]
         S = 1 if cfg.solo else 2
         bcap = tr.max_bullets(idx) + 2
         B = tr.batch_in(idx, S, b_cap=bcap)
-        env = _env(cfg, idx.size, dtype=dtype, b_cap=bcap)
+        env = _env(cfg, idx.size, dtype=dtype, b_cap=bcap, kernel=kernel)
         env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
         ctl = tr.z['control'][idx, :S].astype(np.int8)
         _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
@@ -110,7 +114,8 @@ def test_step_teacher_forced_vs_reference(fname, dtype):
 
 # ------------------------------------------------------- free-running games
 
-def test_whole_games_float64_bit_exact():
+@pytest.mark.parametrize('kernel', KERNELS)
+def test_whole_games_float64_bit_exact(kernel):
     """Every golden game replayed from create(seed) with its open-loop
     controls: every tick's ship state, bullet count, the game length and the
     outcome match the reference bit for bit."""
@@ -121,7 +126,7 @@ def test_whole_games_float64_bit_exact():
     for name, gs in by_cfg.items():
         cfg = CFG[name]
         S = 1 if cfg.solo else 2
-        env = _env(cfg, len(gs), dtype=torch.float64, b_cap=512)
+        env = _env(cfg, len(gs), dtype=torch.float64, b_cap=512, kernel=kernel)
         env.reset(seeds=np.array([g['seed'] for g in gs], dtype=np.uint32))
         T = max(g['ships'].shape[0] for g in gs)
         alive = np.ones(len(gs), bool)
@@ -152,15 +157,16 @@ def test_whole_games_float64_bit_exact():
 
 # ----------------------------------------- batched run vs oracle, auto-reset
 
+@pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('name,n,ticks,bcap', [('default', 4096, 60, 32), ('mp8', 2000, 40, 32),
                                               ('rapid', 512, 30, 6), ('solo', 700, 40, 32)])
-def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap):
+def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap, kernel):
     """N envs with auto-reset, float32 state: every tick equals the oracle
     stepped from the kernel's own input state, resets draw the right seeds
     and create the right games, overflow (small b_cap) is counted alike."""
     cfg = CFG[name]
     P = batched.make_params(cfg)
-    env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, auto_reset=True)
+    env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, auto_reset=True, kernel=kernel)
     env.reset()
     seeds = batched.game_seeds(env.stream_seeds, 64)
     games = np.ones(n, np.int64)          # game 0 was created by reset()
@@ -189,10 +195,11 @@ def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap):
 
 # ------------------------------------------------------- shapes / edge cases
 
-@pytest.mark.parametrize('n', [1, 63, 65, 1000])
-def test_ragged_env_counts(n):
+@pytest.mark.parametrize('kernel', KERNELS)
+@pytest.mark.parametrize('n', [1, 15, 17, 63, 65, 1000])
+def test_ragged_env_counts(n, kernel):
     cfg = CFG['default']
-    env = _env(cfg, n, dtype=torch.float32, b_cap=32, auto_reset=True)
+    env = _env(cfg, n, dtype=torch.float32, b_cap=32, auto_reset=True, kernel=kernel)
     env.reset()
     P = batched.make_params(cfg)
     B = _host_batch(env)
@@ -203,9 +210,10 @@ def test_ragged_env_counts(n):
     _assert_same('n=%d' % n, _host_batch(env), want, wdone == 0, rounding=True)
 
 
-def test_zero_envs_is_a_noop():
+@pytest.mark.parametrize('kernel', KERNELS)
+def test_zero_envs_is_a_noop(kernel):
     cfg = CFG['default']
-    env = _env(cfg, 0, dtype=torch.float32)
+    env = _env(cfg, 0, dtype=torch.float32, kernel=kernel)
     env.reset()
     env.step(torch.zeros((0, 2), dtype=torch.int8, device='cuda'))
     torch.cuda.synchronize()
@@ -235,15 +243,20 @@ def test_full_size_determinism_and_shard_invariance():
     g = torch.Generator(device='cuda').manual_seed(0)
     ctls = torch.randint(0, 6, (ticks, n, 2), generator=g, device='cuda', dtype=torch.int8)
 
-    def run(offset, count):
+    def run(offset, count, kernel='auto'):
         from astro_amd import BatchedEnv
-        env = BatchedEnv(cfg, count, device='cuda:0', b_cap=32, env_offset=offset)
+        env = BatchedEnv(cfg, count, device='cuda:0', b_cap=32, env_offset=offset, kernel=kernel)
         env.reset()
         for t in range(ticks):
             env.step(ctls[t, offset:offset + count].contiguous())
         return env
     a = run(0, n)
     b = run(0, n)
+    c = run(0, n, kernel='lane')
+    d = run(0, n, kernel='quad')
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
+        assert torch.equal(getattr(a, f), getattr(c, f)), f
+        assert torch.equal(getattr(a, f), getattr(d, f)), f
     for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
     lo = run(0, n // 2)
@@ -257,8 +270,9 @@ def test_full_size_determinism_and_shard_invariance():
     assert st['resets'] == st['collisions'] + st['timeouts'] > 0
 
 
+@pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('tick', [0, 7])
-def test_near_threshold_collisions_exact(tick):
+def test_near_threshold_collisions_exact(tick, kernel):
     """Bodies placed within +-2e-4 (relative) of every collision threshold
     (ship-ship, ship-planet, ship-bullet, bullet-planet), at tick 0 (float32
     distances) and later (float64): hit flags, rewards and bullet survival
@@ -296,7 +310,7 @@ def test_near_threshold_collisions_exact(tick):
     for f in ('ships', 'ships_b', 'planets', 'bullets'):
         a = getattr(B, f)
         a[:] = a.astype(np.float32).astype(np.float64)
-    env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, p_pad=4)
+    env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, p_pad=4, kernel=kernel)
     env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
     ctl = rng.randint(0, 6, size=(n, 2)).astype(np.int8)
     want, wrew, wdone = batched.step(B, ctl, P, store='f32')

@@ -47,11 +47,16 @@ def run(name, cfg, n, ticks=200, warm=150, b_cap=32, p_pad=4, auto_reset=True, s
                           planets_per_env=d['planets'] / n)), flush=True)
 
 
-def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4):
-    """Per-section cycle shares from the -DASTRO_STAMPS diagnostic library."""
+def use_lib(name):
     from astro_amd import _lib
     _lib._lib = None
-    _lib.load(os.path.join(ROOT, 'astro_amd', 'libastro_hip_stamps.so'))
+    _lib.load(os.path.join(ROOT, 'astro_amd', name))
+
+
+def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hip_stamps.so'):
+    """Per-section cycle shares from the -DASTRO_STAMPS diagnostic library."""
+    from astro_amd import _lib
+    use_lib(lib)
     env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad)
     env.reset()
     nw = (n + 63) // 64
@@ -85,8 +90,24 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--set', default='basic')
+    ap.add_argument('--libs', default='libastro_hip,libastro_hip_varB')
     a = ap.parse_args()
     D = DEFAULT_CONFIG
+    if a.set == 'epw':
+        for lib in a.libs.split(','):
+            use_lib(lib + '.so')
+            run(lib + ':c3', D, 65536)
+            run(lib + ':c2_noreset', D._replace(reload_time=1000), 65536, auto_reset=False)
+            run(lib + ':c3_262k', D, 262144)
+        return
+    if a.set == 'variants':
+        for lib in a.libs.split(','):
+            use_lib(lib + '.so')
+            run(lib + ':c3', D, 65536)
+            run(lib + ':c2', D._replace(reload_time=1000), 65536)
+            run(lib + ':c3_noreset', D, 65536, auto_reset=False)
+            stamps(lib + ':c3', D, 65536, lib=lib + '_stamps.so')
+        return
     if a.set == 'stamps':
         stamps('c3', D, 65536)
         stamps('c2', D._replace(reload_time=1000), 65536)
