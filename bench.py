@@ -107,6 +107,11 @@ def main():
     ap.add_argument('--cpu-procs', type=int, default=1)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--traffic', default='', help='JSON with PMC-measured HBM bytes per launch')
+    ap.add_argument('--kernel', default='auto', choices=['auto', 'lane', 'quad'])
+    ap.add_argument('--graph', type=int, default=100,
+                    help='launches per captured hipGraph in the timed region (0 = eager launches)')
+    ap.add_argument('--calib', type=int, default=100,
+                    help='eager launches timed one by one (hipEvent pairs) for the kernel duration')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -126,7 +131,7 @@ def main():
     offset = rank * n
     env = BatchedEnv(cfg, n, device=dev, b_cap=wl['b_cap'], p_pad=wl['p_pad'],
                      dtype=torch.float64 if args.state == 'f64' else torch.float32,
-                     env_offset=offset, auto_reset=True)
+                     env_offset=offset, auto_reset=True, kernel=args.kernel)
     env.reset()
     ticks = args.warmup + args.steps
     ctl = torch.from_numpy(controls(offset, n, env.S, ticks)).to(dev)
@@ -142,21 +147,53 @@ def main():
     for t in range(args.warmup):
         env.launch(ptrs[t])
     barrier()
-    s0 = env.stat_dict()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+
+    # Timed region: every one of the K launches has its own control buffer;
+    # with --graph G they are captured G at a time into hipGraphs (capture
+    # launches nothing) so the host's per-launch cost is out of the loop.
+    graphs = []
+    if args.graph > 0:
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(stream)
+        with torch.cuda.stream(cap):
+            for g0 in range(0, args.steps, args.graph):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=cap):
+                    for k in range(g0, min(args.steps, g0 + args.graph)):
+                        env.launch(ptrs[args.warmup + k])
+                graphs.append(g)
+        stream.wait_stream(cap)
     barrier()
+    s0 = env.stat_dict()
+    barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        a, b = evs[k]
-        a.record(stream)
-        env.launch(ptrs[args.warmup + k])
-        b.record(stream)
+    ev0.record(stream)
+    if graphs:
+        for g in graphs:
+            g.replay()
+    else:
+        for k in range(args.steps):
+            env.launch(ptrs[args.warmup + k])
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     barrier()
     s1 = env.stat_dict()
+    gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
+
+    # Kernel duration: launches timed one by one (hipEvent pair around each,
+    # on the launch stream), continuing the same games with fresh controls.
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.calib)]
+    for k in range(args.calib):
+        a, b = evs[k]
+        a.record(stream)
+        env.launch(ptrs[(args.warmup + k) % ticks])
+        b.record(stream)
+    torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
     wall_max = _shard.max_over_ranks(wall, device=dev)
     d = {k: s1[k] - s0[k] for k in s0}
     tot = _shard.sum_over_ranks([d[k] for k in ('bullets_in', 'resets', 'overflows', 'collisions',
@@ -183,7 +220,12 @@ def main():
             roofline=dict(bound='hbm', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
                           frac=achieved / HBM_PEAK_GBS, traffic=traffic,
                           bytes_per_launch=bytes_launch, kernel_ms=kern_ms,
-                          kernel='astro_step_kernel', timing='hipEvent pair per launch'),
+                          kernel='astro_step_%s_kernel' % ('quad' if env.params.kernel == 2 or (
+                              env.params.kernel == 0 and n <= 131072) else 'lane'),
+                          timing='hipEvent pair around each of %d eager launches' % args.calib),
+            gpu_ms_per_step=gpu_ms_per_step,
+            timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph
+                                              if args.graph else 'eager'),
             stats=dict(mean_live_bullets=tot[0] / (n_total * args.steps),
                        resets_per_step=tot[1] / args.steps, overflow_bullets=tot[2],
                        collisions=tot[3], timeouts=tot[4],

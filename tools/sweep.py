@@ -21,9 +21,9 @@ import bench  # noqa: E402
 
 
 def run(name, cfg, n, ticks=200, warm=150, b_cap=32, p_pad=4, auto_reset=True, stats=True,
-        dtype=torch.float32):
+        dtype=torch.float32, kernel='auto'):
     env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, dtype=dtype,
-                     auto_reset=auto_reset)
+                     auto_reset=auto_reset, kernel=kernel)
     env.reset()
     ctl = torch.from_numpy(bench.controls(0, n, env.S, warm + ticks)).cuda()
     for t in range(warm):
@@ -93,6 +93,17 @@ def main():
     ap.add_argument('--libs', default='libastro_hip,libastro_hip_varB')
     a = ap.parse_args()
     D = DEFAULT_CONFIG
+    if a.set == 'kernels':
+        for k in ('lane', 'quad'):
+            run(k + ':c3', D, 65536, kernel=k)
+            run(k + ':c3_noreset', D, 65536, auto_reset=False, kernel=k)
+            run(k + ':c2', D._replace(reload_time=1000), 65536, kernel=k)
+            run(k + ':c3_16k', D, 16384, kernel=k)
+            run(k + ':c3_131k', D, 131072, kernel=k)
+            run(k + ':c3_262k', D, 262144, kernel=k)
+            run(k + ':c3_f64', D, 65536, dtype=torch.float64, kernel=k)
+            run(k + ':c5', D._replace(max_planets=8), 131072, p_pad=8, kernel=k)
+        return
     if a.set == 'epw':
         for lib in a.libs.split(','):
             use_lib(lib + '.so')
