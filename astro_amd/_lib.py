@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'reserved')
@@ -44,6 +44,7 @@ class AstroParams(ctypes.Structure):
         ('fire_bits', ctypes.c_void_p),
         ('kernel', ctypes.c_int32),
         ('reserved', ctypes.c_int32),
+        ('key_table', ctypes.c_void_p),
     ]
 
 
@@ -70,6 +71,8 @@ _SYMBOLS = {
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'astro_stream_init': (ctypes.c_int, [ctypes.POINTER(AstroState), ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    'astro_keytable_build': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_void_p]),
 }
 
 _lib = None

@@ -34,7 +34,7 @@ def _env(config, bullets_needed):
         while cap < bullets_needed:
             cap *= 2
         env = BatchedEnv(config, 1, device=key[1], b_cap=cap, dtype=torch.float64,
-                         auto_reset=False)
+                         auto_reset=False, use_key_table=False)
         env._fire = torch.zeros(2, dtype=torch.int32, device=key[1])
         _ENVS[key] = env
     return env

@@ -247,22 +247,21 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 }
 
 // key[to] of init_genrand given key[from] = v: the 397-step sequential chain
-// every RandomState(seed) pays before its first output
+// every RandomState(seed) pays before its first output.  Each step is a
+// dependent xor-shift + v_mul_lo_u32 + add, ~50 cycles of latency on gfx950,
+// so a whole chain is ~9 us for a lone lane -- hence the key table below.
 __device__ __forceinline__ uint32_t mt_key_at(uint32_t v, uint32_t from, uint32_t to) {
     for (uint32_t k = from + 1; k <= to; ++k) v = mt_key_next(v, k);
     return v;
 }
 
 constexpr uint32_t MT_PROLOGUE = 397;
-// Amortised seeding: every running env advances the init chain of its NEXT
-// game's seed by this many steps per tick, so a game that ends after
-// >= 397/8 = 50 ticks re-creates without paying the chain (a wave otherwise
-// stalls on whichever of its 64 games ended).
-constexpr uint32_t MT_STEPS_PER_TICK = 8;
 
-// hdr word 0 = tick | pending-chain progress << 22
+// hdr word 0 = tick | KEY_VALID (hdr word 3 holds key[397] of the pending seed)
 constexpr int TICK_BITS = 22;
 constexpr uint32_t TICK_MASK = (1u << TICK_BITS) - 1;
+constexpr uint32_t KEY_VALID = 1u << 31;
+constexpr uint32_t SEED_MASK = (1u << 30) - 1;   // generate_configs seeds are randint(1 << 30)
 
 struct MTLazy {
     uint32_t a;  // key[i]
@@ -311,6 +310,14 @@ struct MTLazy {
     }
 };
 
+// key[397] of RandomState(seed)'s init chain: one gather from the device
+// table (every 30-bit seed, built once by astro_keytable_build) or, without
+// a table / for a wider explicit seed, the chain itself.
+__device__ __forceinline__ uint32_t key397_of(const AstroParams &p, uint32_t seed) {
+    if (p.key_table && seed <= SEED_MASK) return p.key_table[seed];
+    return mt_key_at(seed, 0, MT_PROLOGUE);
+}
+
 constexpr double TWO_PI = 6.283185307179586;  // 2 * np.pi
 constexpr double PI = 3.141592653589793;      // np.pi
 
@@ -326,6 +333,23 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
     T *ships_b = reinterpret_cast<T *>(st.ships_b);
     V *planets = reinterpret_cast<V *>(st.planets);
 
+#ifdef ASTRO_STUB_CREATE   // timing experiment only: a fixed 3-planet game, no RNG/trig
+    {
+        V v;
+        v.z = v.w = T(0);
+        v.x = T(0.9f); v.y = T(-0.9f); ships[i] = v; ships_b[i] = T(1.0f);
+        if (S == 2) { v.x = T(-0.2f); v.y = T(0.1f); ships[N + i] = v; ships_b[N + i] = T(2.0f); }
+        const float px[3] = {0.5f, -0.25f, -0.25f}, py[3] = {0.0f, 0.433f, -0.433f};
+        for (int j = 0; j < 3 && j < PMAX; ++j) {
+            V w;
+            w.x = T(px[j]); w.y = T(py[j]); w.z = T(-0.1f * py[j]); w.w = T(0.1f * px[j]);
+            planets[size_t(j) * N + i] = w;
+        }
+        flags_out = 0;
+        (void)seed; (void)key397;
+        return PMAX < 3 ? PMAX : 3;
+    }
+#endif
     MTLazy g;
     g.seed_from(seed, key397);
     int n = g.randint(1, p.max_planets + 1);
@@ -405,13 +429,15 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
 // partially advanced init chain (.z, progress in .x >> 22), so a reset can
 // start creating before the cold stream record arrives.
 
-// Start env i's next game: finish the pending seed's chain (usually done
-// already), create, draw the seed after it.
+// Start env i's next game: its seed was drawn one game ahead (hdr word 2) and
+// key[397] of that seed fetched from the key table by an earlier step (hdr
+// word 3, valid when KEY_VALID); create, then draw the following seed.  The
+// following seed's key is gathered by the NEXT step, off this path.
 template <typename T, int S, int PMAX>
 __device__ __forceinline__ void restart_from_stream(const AstroParams &p, const AstroState &st, int i,
-                                                    uint32_t pend_v, uint32_t pend_j, uint32_t pend_seed) {
+                                                    uint32_t pend_seed, uint32_t pend_key, bool key_valid) {
     uint4 c = reinterpret_cast<uint4 *>(st.stream)[i];   // in flight during create
-    const uint32_t key397 = mt_key_at(pend_v, pend_j, MT_PROLOGUE);
+    const uint32_t key397 = key_valid ? pend_key : key397_of(p, pend_seed);
     int cf = 0;
     const int n = create_env<T, S, PMAX>(p, st, i, pend_seed, key397, cf);
     MTLazy g;
@@ -419,10 +445,10 @@ __device__ __forceinline__ void restart_from_stream(const AstroParams &p, const 
     g.b = c.y;
     g.i = c.z;
     const bool exhausted = !g.ok();
-    const uint32_t next_seed = g.next() & ((1u << 30) - 1);
+    const uint32_t next_seed = g.next() & SEED_MASK;
     reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, pend_seed);
     const int flags = (exhausted || cf) ? 2 : 0;
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(next_seed), int(next_seed));
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(next_seed), 0);
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -623,8 +649,8 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             ctl[0] = int(control[i]);
         }
         const int tick = int(uint32_t(h.x) & TICK_MASK);
-        const uint32_t pend_j = uint32_t(h.x) >> TICK_BITS;
-        const uint32_t pend_v = uint32_t(h.z);
+        const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
+        const uint32_t pend_seed = uint32_t(h.z);
         int np = h.y & 0xff;
         int flags = (h.y >> 8) & 0xff;
         const int nb = int(uint32_t(h.y) >> 16);
@@ -646,6 +672,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             pdy[j] = double(v.w);
         }
         const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
+        // key[397] of the next game's seed, fetched once per game, off the reset path
+        uint32_t pend_key = uint32_t(h.w);
+        if (!key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
         V buf[BCHUNK];
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) {
@@ -815,18 +844,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             }
             STAMP(7);
             if (dropped) flags |= 1;
-            // advance the next game's init chain (amortised seeding)
-            uint32_t v = pend_v, j = pend_j;
-#pragma unroll
-            for (uint32_t k = 0; k < MT_STEPS_PER_TICK; ++k) {
-                if (j < MT_PROLOGUE) {
-                    ++j;
-                    v = mt_key_next(v, j);
-                }
-            }
+            const uint32_t kv = (key_valid || p.key_table) ? KEY_VALID : 0u;
             reinterpret_cast<int4 *>(st.hdr)[i] =
-                make_int4(int(uint32_t(tick + 1) | (j << TICK_BITS)), np | (flags << 8) | (w << 16), int(v), h.w);
-
+                make_int4(int(uint32_t(tick + 1) | kv), np | (flags << 8) | (w << 16), int(pend_seed), int(pend_key));
             n_bout = uint32_t(w);
             n_drop = uint32_t(dropped);
             STAMP(8);
@@ -835,7 +855,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             f_coll = collided;
             f_tout = timeout;
             if (auto_reset) {
-                restart_from_stream<T, S, PMAX>(p, st, i, pend_v, pend_j, uint32_t(h.w));
+                restart_from_stream<T, S, PMAX>(p, st, i, pend_seed, pend_key, key_valid || p.key_table);
                 f_reset = true;
             }
             STAMP(10);
@@ -951,8 +971,8 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
         const T sbv = ships_b[size_t(sq) * NN + i];
         const int ctl = int(control[size_t(i) * S + sq]);
         const int tick = int(uint32_t(h.x) & TICK_MASK);
-        const uint32_t pend_j = uint32_t(h.x) >> TICK_BITS;
-        const uint32_t pend_v = uint32_t(h.z);
+        const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
+        const uint32_t pend_seed = uint32_t(h.z);
         int np = h.y & 0xff;
         int flags = (h.y >> 8) & 0xff;
         const int nb = int(uint32_t(h.y) >> 16);
@@ -971,6 +991,8 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
             mpy[m] = pv[m].y;
         }
         const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
+        uint32_t pend_key = uint32_t(h.w);
+        if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
         const int rounds = (nb + 3) >> 2;
         V cur[QB];
 #pragma unroll
@@ -1243,16 +1265,9 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
 
             if (q == 0) {
                 const int fl = flags | (dropped ? 1 : 0);
-                uint32_t v = pend_v, j = pend_j;
-#pragma unroll
-                for (uint32_t k = 0; k < MT_STEPS_PER_TICK; ++k) {
-                    if (j < MT_PROLOGUE) {
-                        ++j;
-                        v = mt_key_next(v, j);
-                    }
-                }
+                const uint32_t kv = (key_valid || p.key_table) ? KEY_VALID : 0u;
                 reinterpret_cast<int4 *>(st.hdr)[i] =
-                    make_int4(int(uint32_t(tick + 1) | (j << TICK_BITS)), np | (fl << 8) | (w << 16), int(v), h.w);
+                    make_int4(int(uint32_t(tick + 1) | kv), np | (fl << 8) | (w << 16), int(pend_seed), int(pend_key));
                 n_bout = uint32_t(w);
                 n_drop = uint32_t(dropped);
             }
@@ -1260,7 +1275,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
             f_coll = collided;
             f_tout = timeout;
             if (auto_reset) {
-                restart_from_stream<T, S, PMAX>(p, st, i, pend_v, pend_j, uint32_t(h.w));
+                restart_from_stream<T, S, PMAX>(p, st, i, pend_seed, pend_key, key_valid || p.key_table);
                 f_reset = true;
             }
         }
@@ -1298,13 +1313,13 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
     if (mask && !mask[i]) return;
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
     if (!seeds) {
-        restart_from_stream<T, S, PMAX>(p, st, i, uint32_t(h.z), uint32_t(h.x) >> TICK_BITS, uint32_t(h.w));
+        restart_from_stream<T, S, PMAX>(p, st, i, uint32_t(h.z), uint32_t(h.w), (uint32_t(h.x) & KEY_VALID) != 0);
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued
     int cf = 0;
     const uint32_t seed = seeds[i];
-    const int n = create_env<T, S, PMAX>(p, st, i, seed, mt_key_at(seed, 0, MT_PROLOGUE), cf);
+    const int n = create_env<T, S, PMAX>(p, st, i, seed, key397_of(p, seed), cf);
     reinterpret_cast<int4 *>(st.hdr)[i] =
         make_int4(int(uint32_t(h.x) & ~TICK_MASK), n | ((cf ? 2 : 0) << 8), h.z, h.w);
     if (st.stream) reinterpret_cast<uint32_t *>(st.stream)[4 * i + 3] = seed;
@@ -1318,7 +1333,29 @@ __global__ __launch_bounds__(BLOCK) void astro_stream_init_kernel(AstroState st,
     g.seed(seeds[i]);
     const uint32_t first = g.next() & ((1u << 30) - 1);   // game 0's seed, pending
     reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, 0u);
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, 1, int(first), int(first));
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, 1, int(first), 0);
+}
+
+// key[397] for seeds first .. first+count-1; four independent chains per
+// lane so the ~50-cycle step latency overlaps
+__global__ __launch_bounds__(256) void astro_keytable_kernel(uint32_t *__restrict__ table, uint32_t first,
+                                                             uint32_t count) {
+    const uint32_t lanes = gridDim.x * 256u;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    for (uint32_t base = t; base < count; base += 4u * lanes) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = first + base + uint32_t(u) * lanes;
+        for (uint32_t k = 1; k <= MT_PROLOGUE; ++k) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = mt_key_next(v[u], k);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t idx = base + uint32_t(u) * lanes;
+            if (idx < count) table[first + idx] = v[u];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1467,6 +1504,17 @@ int astro_reset(const AstroParams *p, const AstroState *s, const uint32_t *seeds
     if (s->n_env == 0) return 0;
     if (!seeds && !s->stream) return fail(-40, "reset without seeds needs the stream array");
     return dispatch<ResetL>(*p, *s, seeds, mask, reinterpret_cast<hipStream_t>(stream));
+}
+
+int astro_keytable_build(uint32_t *table, uint32_t first, uint32_t count, void *stream) {
+    if (!table) return fail(-50, "table is NULL");
+    if (uint64_t(first) + count > (uint64_t(1) << 30)) return fail(-51, "key table covers seeds < 2^30");
+    if (count == 0) return 0;
+    const uint32_t lanes_needed = (count + 3) / 4;
+    const uint32_t grid = (lanes_needed + 255) / 256 < 65536u ? (lanes_needed + 255) / 256 : 65536u;
+    hipLaunchKernelGGL(astro_keytable_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       table, first, count);
+    return launched("astro_keytable_build");
 }
 
 int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *stream) {

@@ -41,6 +41,26 @@ def _stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+_KEY_TABLES = {}
+KEY_TABLE_SEEDS = 1 << 30
+
+
+def key_table(device):
+    """The per-device table of key[397] of MT19937 init_genrand for every
+    30-bit seed (4 GiB, built once per process and device in ~0.1 s): it
+    turns each game's 397-step seeding chain into one gather."""
+    device = torch.device(device)
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    t = _KEY_TABLES.get(key)
+    if t is None:
+        lib = _lib.load()
+        t = torch.empty(KEY_TABLE_SEEDS, dtype=torch.int32, device=device)
+        _lib.check(lib.astro_keytable_build(t.data_ptr(), 0, KEY_TABLE_SEEDS, _stream_ptr(device)),
+                   'astro_keytable_build')
+        _KEY_TABLES[key] = t
+    return t
+
+
 class BatchedEnv:
     """N lockstep games of one Config on one device.
 
@@ -53,10 +73,13 @@ class BatchedEnv:
     env_offset -- global id of env 0 (multi-GPU sharding)
     kernel     -- 'auto', 'lane' (one lane per env) or 'quad' (four lanes
                   per env); identical results, different speed
+    use_key_table -- share the device's 4 GiB seeding table (see key_table);
+                  False runs every game's 397-step chain inline (same results)
     """
 
     def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
-                 dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto'):
+                 dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto',
+                 use_key_table=True):
         _schedule.check_config(config)
         if dtype not in (torch.float32, torch.float64):
             raise ValueError('dtype must be torch.float32 or torch.float64')
@@ -90,9 +113,11 @@ class BatchedEnv:
         self.fire_bits = torch.from_numpy(self.schedule.fire_bits().view(np.int32)).to(dev)
 
         k = _schedule.kernel_constants(config)
+        self.key_table = key_table(dev) if use_key_table else None
         self.params = _lib.AstroParams(
             p_pad=self.p_pad, b_cap=self.b_cap, timeout_tick=self.schedule.timeout_tick,
-            fire_bits=self.fire_bits.data_ptr(), kernel=_lib.KERNELS[kernel], **k)
+            fire_bits=self.fire_bits.data_ptr(), kernel=_lib.KERNELS[kernel],
+            key_table=self.key_table.data_ptr() if self.key_table is not None else None, **k)
         self.state = _lib.AstroState(
             ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),
             planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),
@@ -219,7 +244,7 @@ class BatchedEnv:
             raise ValueError('a state holds more bullets than b_cap')
         old = self.hdr.cpu().numpy().view(np.uint32).astype(np.int64)
         hdr = old.copy()
-        hdr[:, 0] = (old[:, 0] & ~TICK_MASK) | np.asarray(tick, np.int64)
+        hdr[:, 0] = (old[:, 0] & ~TICK_MASK & 0xFFFFFFFF) | np.asarray(tick, np.int64)
         hdr[:, 1] = np.asarray(nplanets, np.int64) | (nb << 16)
         self.hdr.copy_(torch.as_tensor(hdr.astype(np.uint32).view(np.int32)).to(dev))
 

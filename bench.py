@@ -220,8 +220,8 @@ def main():
             roofline=dict(bound='hbm', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
                           frac=achieved / HBM_PEAK_GBS, traffic=traffic,
                           bytes_per_launch=bytes_launch, kernel_ms=kern_ms,
-                          kernel='astro_step_%s_kernel' % ('quad' if env.params.kernel == 2 or (
-                              env.params.kernel == 0 and n <= 131072) else 'lane'),
+                          kernel=('astro_step_quad_kernel' if env.params.kernel == 2 or (
+                              env.params.kernel == 0 and n <= 131072) else 'astro_step_kernel'),
                           timing='hipEvent pair around each of %d eager launches' % args.calib),
             gpu_ms_per_step=gpu_ms_per_step,
             timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 3
+#define ASTRO_ABI_VERSION 4
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -64,6 +64,9 @@ typedef struct AstroParams {
     const uint32_t *fire_bits; /* device: bit k = fire on tick k, k < timeout_tick */
     int32_t kernel;        /* ASTRO_KERNEL_AUTO / _LANE / _QUAD (results are identical) */
     int32_t reserved;
+    const uint32_t *key_table; /* device, optional: key[397] of MT19937 init_genrand for
+                                  every seed < 2^30 (astro_keytable_build); NULL = the
+                                  397-step chain at each create (~9 us per lane) */
 } AstroParams;
 
 /* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:
@@ -73,14 +76,14 @@ enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2 };
 #define ASTRO_QUAD_MAX_ENVS 131072
 
 /* Per-env state arrays (device pointers).  hdr packs
- *   hdr[4*i+0] = tick (steps since create, < 2^22) | chain progress j << 22
+ *   hdr[4*i+0] = tick (steps since create, < 2^22) | key_valid << 31
  *   hdr[4*i+1] = nplanets | flags << 8 | nbullets << 16
- *   hdr[4*i+2] = key[j] of the NEXT game's MT19937 init chain
- *   hdr[4*i+3] = the NEXT game's seed (drawn one game ahead from the stream)
+ *   hdr[4*i+2] = the NEXT game's seed (drawn one game ahead from the stream)
+ *   hdr[4*i+3] = key[397] of that seed's MT19937 init chain (when key_valid)
  * flags: bit0 = a bullet was dropped (b_cap full) this game,
  *        bit1 = the env's seed stream ran past its 227 exact games.
- * Every running env advances its next game's 397-step init chain by 8 steps
- * per tick, so an auto-reset normally starts with the chain complete. */
+ * A running step fetches the next game's key[397] from the key table once,
+ * so an auto-reset never runs the 397-step chain inline. */
 typedef struct AstroState {
     void *ships;        /* [nships][n_env][4]  x, y, dx, dy */
     void *ships_b;      /* [nships][n_env]     bearing */
@@ -124,6 +127,10 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
  * seeds[i] when seeds != NULL, else from the next seed of env i's stream. */
 int astro_reset(const AstroParams *p, const AstroState *s, const uint32_t *seeds,
                 const uint8_t *mask, void *stream);
+
+/* Fill table[first .. first+count-1] with key[397] of RandomState(seed)'s
+ * init chain (table: uint32 [2^30] for the full range, 4 GiB; ~0.1 s). */
+int astro_keytable_build(uint32_t *table, uint32_t first, uint32_t count, void *stream);
 
 /* Position env i's seed stream at generate_configs(seed=stream_seeds[i]) and
  * queue its first game (the next astro_reset without seeds creates it). */

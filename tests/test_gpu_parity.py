@@ -320,3 +320,35 @@ def test_near_threshold_collisions_exact(tick, kernel):
     assert np.array_equal(rew.cpu().numpy(), wrew)
     _assert_same('near-threshold tick=%d' % tick, _host_batch(env), want, wdone == 0, rounding=True)
     assert 0.05 < (wdone == 1).mean() < 0.95   # both outcomes well represented
+
+
+def test_key_table_matches_mt_init_chain():
+    """The device seeding table holds key[397] of init_genrand for every
+    30-bit seed: spot-check against the oracle's MT19937 restatement."""
+    from astro_amd.env import key_table
+    from oracle import mt19937
+    t = key_table('cuda:0')
+    rng = np.random.RandomState(3)
+    seeds = np.concatenate([[0, 1, 42, (1 << 30) - 1], rng.randint(0, 1 << 30, 2000)]).astype(np.uint64)
+    want = mt19937.init_genrand(seeds)[:, 397].astype(np.uint32)
+    got = t[torch.from_numpy(seeds.astype(np.int64)).cuda()].cpu().numpy().view(np.uint32)
+    assert (got == want).all()
+
+
+@pytest.mark.parametrize('kernel', KERNELS)
+def test_without_key_table_identical(kernel):
+    """use_key_table=False (inline 397-step chains) gives the same games."""
+    from astro_amd import BatchedEnv
+    cfg = CFG['default']
+    n, ticks = 2048, 120
+    g = torch.Generator(device='cuda').manual_seed(5)
+    ctls = torch.randint(0, 6, (ticks, n, 2), generator=g, device='cuda', dtype=torch.int8)
+    envs = [BatchedEnv(cfg, n, device='cuda:0', use_key_table=u, kernel=kernel) for u in (True, False)]
+    for e in envs:
+        e.reset()
+        for t in range(ticks):
+            e.step(ctls[t])
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'stream'):
+        assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), f
+    assert torch.equal(envs[0].hdr[:, 1], envs[1].hdr[:, 1])
+    assert envs[0].stat_dict()['resets'] > 0

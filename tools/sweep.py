@@ -93,6 +93,37 @@ def main():
     ap.add_argument('--libs', default='libastro_hip,libastro_hip_varB')
     a = ap.parse_args()
     D = DEFAULT_CONFIG
+    if a.set == 'create':
+        for n in (1024, 65536):
+            env = BatchedEnv(D, n, device='cuda:0')
+            env.reset()
+            torch.cuda.synchronize()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+            for k in range(20):
+                evs[k][0].record()
+                env.reset()
+                evs[k][1].record()
+            torch.cuda.synchronize()
+            ms = np.array([x.elapsed_time(y) for x, y in evs])
+            seeds = np.arange(n, dtype=np.uint32) * 7919 + 13
+            evs2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+            st = torch.from_numpy(seeds.view(np.int32)).cuda()
+            for k in range(20):
+                evs2[k][0].record()
+                env.reset(seeds=st)
+                evs2[k][1].record()
+            torch.cuda.synchronize()
+            ms2 = np.array([x.elapsed_time(y) for x, y in evs2])
+            print(json.dumps(dict(name='reset_stream', n=n, med_us=float(np.median(ms)) * 1e3,
+                                  explicit_seed_med_us=float(np.median(ms2)) * 1e3)), flush=True)
+        return
+    if a.set == 'stub':
+        for lib in a.libs.split(','):
+            use_lib(lib + '.so')
+            for k in ('lane', 'quad'):
+                run(lib + ':' + k + ':c3', D, 65536, kernel=k)
+                run(lib + ':' + k + ':c2', D._replace(reload_time=1000), 65536, kernel=k)
+        return
     if a.set == 'kernels':
         for k in ('lane', 'quad'):
             run(k + ':c3', D, 65536, kernel=k)
