@@ -205,9 +205,13 @@ def main():
         value = n_total * args.steps / wall_max
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
         traffic = None
-        if args.traffic and os.path.exists(args.traffic):
-            with open(args.traffic) as f:
-                traffic = json.load(f).get('hbm_bytes_per_launch')
+        tpath = args.traffic or os.path.join(ROOT, 'profiles', 'round1', 'traffic_%s_%s.json' % (
+            args.workload, args.state))
+        if os.path.exists(tpath):
+            with open(tpath) as f:
+                tj = json.load(f)
+            if tj.get('n_env') == n and tj.get('kernel') in (args.kernel, 'auto'):
+                traffic = tj.get('hbm_bytes_per_launch')
         out = dict(
             metric=METRIC, value=value, unit='env-steps/s', n_gpus=world, steps=args.steps,
             warmup=args.warmup, ms_per_step=wall_max / args.steps * 1e3, higher_is_better=True,
@@ -221,7 +225,7 @@ def main():
                           frac=achieved / HBM_PEAK_GBS, traffic=traffic,
                           bytes_per_launch=bytes_launch, kernel_ms=kern_ms,
                           kernel=('astro_step_quad_kernel' if env.params.kernel == 2 or (
-                              env.params.kernel == 0 and n <= 131072) else 'astro_step_kernel'),
+                              env.params.kernel == 0 and n <= 65536) else 'astro_step_kernel'),
                           timing='hipEvent pair around each of %d eager launches' % args.calib),
             gpu_ms_per_step=gpu_ms_per_step,
             timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph

@@ -73,7 +73,7 @@ typedef struct AstroParams {
  * four lanes per env (16 envs per wave), for batches too small to give each
  * SIMD several waves.  AUTO picks QUAD for n_env <= ASTRO_QUAD_MAX_ENVS. */
 enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2 };
-#define ASTRO_QUAD_MAX_ENVS 131072
+#define ASTRO_QUAD_MAX_ENVS 65536
 
 /* Per-env state arrays (device pointers).  hdr packs
  *   hdr[4*i+0] = tick (steps since create, < 2^22) | key_valid << 31
