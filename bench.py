@@ -203,7 +203,11 @@ def main():
     if rank == 0:
         n_total = n * world
         value = n_total * args.steps / wall_max
-        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+        # per-launch duration = hipEvents bracketing the timed region (the
+        # hipGraph replays) / K; rocprofv3's kernel average agrees within ~2%
+        # (profiles/round1); one event pair per eager launch adds ~2.5 us
+        launch_ms = gpu_ms_per_step
+        achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
         tpath = args.traffic or os.path.join(ROOT, 'profiles', 'round1', 'traffic_%s_%s.json' % (
             args.workload, args.state))
@@ -223,10 +227,11 @@ def main():
                         state=args.state, parallelism='env-shard x%d (no collectives)' % world),
             roofline=dict(bound='hbm', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
                           frac=achieved / HBM_PEAK_GBS, traffic=traffic,
-                          bytes_per_launch=bytes_launch, kernel_ms=kern_ms,
+                          bytes_per_launch=bytes_launch, kernel_ms=launch_ms,
+                          kernel_ms_eager_event_pairs=kern_ms,
                           kernel=('astro_step_quad_kernel' if env.params.kernel == 2 or (
                               env.params.kernel == 0 and n <= 65536) else 'astro_step_kernel'),
-                          timing='hipEvent pair around each of %d eager launches' % args.calib),
+                          timing='hipEvent pair around the timed region / K launches'),
             gpu_ms_per_step=gpu_ms_per_step,
             timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph
                                               if args.graph else 'eager'),
