@@ -28,6 +28,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from . import shard as _shard
 from .config import Bodies, State, nships as _nships
 from . import schedule as _schedule
 
@@ -124,9 +125,7 @@ class BatchedEnv:
             hdr=self.hdr.data_ptr(), stream=self.stream.data_ptr(),
             n_env=N, state_f64=1 if dtype == torch.float64 else 0)
 
-        seeds = np.random.RandomState(config.seed).randint(
-            1 << 30, size=self.env_offset + N)[self.env_offset:]
-        self.stream_seeds = seeds.astype(np.uint32)
+        self.stream_seeds = _shard.stream_seeds(config, self.env_offset, N)
         seeds_t = torch.from_numpy(self.stream_seeds.view(np.int32)).to(dev)
         _lib.check(self.lib.astro_stream_init(ctypes.byref(self.state), seeds_t.data_ptr(),
                                               _stream_ptr(dev)), 'astro_stream_init')

@@ -38,3 +38,13 @@ def sum_over_ranks(values, device=None):
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.tolist()
+
+
+def stream_seeds(config, offset, count):
+    """Seed-stream seeds of global envs offset .. offset+count-1: the first
+    configs of generate_configs(config) (core.py:77-83), i.e.
+    RandomState(config.seed).randint(1 << 30) drawn in sequence.  Host numpy,
+    O(offset + count)."""
+    import numpy as np
+    seeds = np.random.RandomState(config.seed).randint(1 << 30, size=int(offset) + int(count))
+    return seeds[int(offset):].astype(np.uint32)

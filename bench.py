@@ -119,11 +119,18 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal)
+    # ranks share devices and ASTRO_DIST_BACKEND=gloo avoids RCCL's one-rank-per-GPU rule
+    dev = torch.device('cuda', local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    backend = os.environ.get('ASTRO_DIST_BACKEND', 'nccl')
+    red_dev = dev if backend == 'nccl' else None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     wl = WORKLOADS[args.workload]
     cfg = DEFAULT_CONFIG._replace(**wl['cfg'])
@@ -194,10 +201,10 @@ def main():
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
-    wall_max = _shard.max_over_ranks(wall, device=dev)
+    wall_max = _shard.max_over_ranks(wall, device=red_dev)
     d = {k: s1[k] - s0[k] for k in s0}
     tot = _shard.sum_over_ranks([d[k] for k in ('bullets_in', 'resets', 'overflows', 'collisions',
-                                                'timeouts')], device=dev)
+                                                'timeouts')], device=red_dev)
     bytes_launch = algorithmic_bytes(env, d, args.steps)
 
     if rank == 0:
