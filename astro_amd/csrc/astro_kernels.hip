@@ -136,15 +136,6 @@ __device__ __forceinline__ void field(const double (&px)[PMAX], const double (&p
     gy = ay;
 }
 
-// squared distance of _collisions (core.py:210) in precision C, compared in
-// float64 against the float64 (r_i + r_j)^2
-template <typename C>
-__device__ __forceinline__ double dist2(double ax, double ay, double bx, double by) {
-    const C dx = C(ax) - C(bx);
-    const C dy = C(ay) - C(by);
-    return double(dx * dx + dy * dy);
-}
-
 // Collision test |a - b|^2 < r2 of _collisions (core.py:210-212), exact,
 // branch-free.  At tick 0 the reference evaluates the distance in float32
 // (create's float32 arrays) and that float32 value IS the answer; float
@@ -165,13 +156,32 @@ struct Guard {
     }
 };
 
-__device__ __forceinline__ bool closer32(float ax, float ay, float bx, float by, const Guard &g, bool t0,
-                                         bool valid, bool &amb) {
+// The common-case test against the uniform thresholds (SGPRs): hit <=>
+// d2 < lo; a d2 inside [lo, hi] is ambiguous.  Tick 0 is not decided here:
+// callers flag tick-0 lanes ambiguous and decide them on the exact path.
+// Invalid operands are parked at FAR_POS / -FAR_POS: their d2 is +inf, which
+// neither hits nor lands in the band.
+constexpr float FAR_POS = 1e30f;
+
+__device__ __forceinline__ bool near32(float ax, float ay, float bx, float by, const Guard &g, bool &amb) {
     const float dx = ax - bx;
     const float dy = ay - by;
     const float d2 = dx * dx + dy * dy;
-    amb |= valid & !t0 & (d2 >= g.lo) & (d2 <= g.hi);
-    return valid & (t0 ? d2 <= g.t0_max : d2 < g.lo);
+    amb |= (d2 >= g.lo) & (d2 <= g.hi);
+    return d2 < g.lo;
+}
+
+// the exact test of the ambiguous path: at tick 0 the float32 distance of
+// create()'s float32 arrays, later float64
+__device__ __forceinline__ bool closer_exact(double ax, double ay, double bx, double by, const Guard &g, bool t0) {
+    if (t0) {
+        const float dx = float(ax) - float(bx);
+        const float dy = float(ay) - float(by);
+        return dx * dx + dy * dy <= g.t0_max;
+    }
+    const double dx = ax - bx;
+    const double dy = ay - by;
+    return dx * dx + dy * dy < g.r2;
 }
 
 // Planet-on-planet gravity (core.py:291) for every planet i < np, in the
@@ -323,10 +333,13 @@ constexpr double PI = 3.141592653589793;      // np.pi
 
 // ---------------------------------------------------------------------------
 // create() (core.py:86-135) for env i from `seed`; writes the env's slots.
+// NPART lanes may share one env: each runs the (cheap, serial) random draws
+// and writes ships s and planets j with s, j = part mod NPART, so the
+// trigonometry of the planets runs in parallel.
 
-template <typename T, int S, int PMAX>
+template <typename T, int S, int PMAX, int NPART = 1>
 __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uint32_t seed, uint32_t key397,
-                          int &flags_out) {
+                          int &flags_out, int part = 0) {
     using V = typename Store<T>::V;
     const size_t N = size_t(st.n_env);
     V *ships = reinterpret_cast<V *>(st.ships);
@@ -389,13 +402,15 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
         v.y = T(shy[s]);
         v.z = T(0);
         v.w = T(0);
-        ships[size_t(s) * N + i] = v;
-        ships_b[size_t(s) * N + i] = T(b);
+        if (s % NPART == part) {
+            ships[size_t(s) * N + i] = v;
+            ships_b[size_t(s) * N + i] = T(b);
+        }
     }
     if (n == 1) {
         V v;
         v.x = v.y = v.z = v.w = T(0);
-        planets[i] = v;
+        if (part == 0) planets[i] = v;
     } else {
         const double base = TWO_PI * g.rand();
         const double stp = TWO_PI / double(n);
@@ -403,7 +418,8 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
         const double amp = sqrt(p.gravity * p.planet_mass * double(n - 1) / 2.0);
         const double turn = double(reverse) * PI / 2.0;
 #pragma unroll
-        for (int j = 0; j < PMAX; ++j) {
+        for (int m = 0; m < PMAX / NPART; ++m) {
+            const int j = part + NPART * m;
             if (j >= n) continue;
             const double orient = base + double(j) * stp;
             float ps, pc, vs, vc;
@@ -433,13 +449,15 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
 // key[397] of that seed fetched from the key table by an earlier step (hdr
 // word 3, valid when KEY_VALID); create, then draw the following seed.  The
 // following seed's key is gathered by the NEXT step, off this path.
-template <typename T, int S, int PMAX>
+template <typename T, int S, int PMAX, int NPART = 1>
 __device__ __forceinline__ void restart_from_stream(const AstroParams &p, const AstroState &st, int i,
-                                                    uint32_t pend_seed, uint32_t pend_key, bool key_valid) {
+                                                    uint32_t pend_seed, uint32_t pend_key, bool key_valid,
+                                                    int part = 0) {
     uint4 c = reinterpret_cast<uint4 *>(st.stream)[i];   // in flight during create
     const uint32_t key397 = key_valid ? pend_key : key397_of(p, pend_seed);
     int cf = 0;
-    const int n = create_env<T, S, PMAX>(p, st, i, pend_seed, key397, cf);
+    const int n = create_env<T, S, PMAX, NPART>(p, st, i, pend_seed, key397, cf, part);
+    if (part != 0) return;
     MTLazy g;
     g.a = c.x;
     g.b = c.y;
@@ -488,7 +506,7 @@ constexpr int BCHUNK = 8;  // bullets loaded per batch: 8 loads in flight per la
 // with BOTH coordinates outside [-1, 1] (core.py:295-300, 195), compacting in
 // order, in place (slot written <= slot read).
 template <typename C, typename T, int S, int PMAX>
-__device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store<T>::V *bullets, size_t NN, int i,
+__device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store<T>::V *bullets, size_t BC, int i,
                                             int nb, int np, const double (&px)[PMAX], const double (&py)[PMAX],
                                             const double (&sx)[S], const double (&sy)[S],
                                             typename Store<T>::V (&cur)[BCHUNK], bool (&hit)[S], int &w,
@@ -496,11 +514,11 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
     using V = typename Store<T>::V;
     const C dt = C(p.dt);
     const Guard gp(p.r2_p0), gs(p.r2_s0);
-    float pxf[PMAX], pyf[PMAX], sxf[S], syf[S];
+    float pxf[PMAX], pyf[PMAX], sxf[S], syf[S];   // float32 copies, padding parked far away
 #pragma unroll
     for (int j = 0; j < PMAX; ++j) {
-        pxf[j] = float(px[j]);
-        pyf[j] = float(py[j]);
+        pxf[j] = j < np ? float(px[j]) : -FAR_POS;
+        pyf[j] = j < np ? float(py[j]) : -FAR_POS;
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -515,7 +533,7 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
 #pragma unroll
             for (int u = 0; u < BCHUNK; ++u) {
                 const int k = base + BCHUNK + u < nb ? base + BCHUNK + u : 0;
-                nxt[u] = bullets[size_t(k) * NN + i];
+                nxt[u] = bullets[size_t(i) * BC + k];
             }
         }
 #pragma unroll
@@ -525,21 +543,22 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
             // recheck are conditional
             const bool valid = base + u < nb;
             const double x = double(cur[u].x), y = double(cur[u].y);
-            const float xf = float(cur[u].x), yf = float(cur[u].y);
+            const float xf = valid ? float(cur[u].x) : FAR_POS, yf = valid ? float(cur[u].y) : FAR_POS;
             bool bh = false, amb = false, hs[S];
 #pragma unroll
-            for (int j = 0; j < PMAX; ++j) bh |= closer32(xf, yf, pxf[j], pyf[j], gp, t0, valid & (j < np), amb);
+            for (int j = 0; j < PMAX; ++j) bh |= near32(xf, yf, pxf[j], pyf[j], gp, amb);
 #pragma unroll
-            for (int s = 0; s < S; ++s) hs[s] = closer32(xf, yf, sxf[s], syf[s], gs, t0, valid, amb);
+            for (int s = 0; s < S; ++s) hs[s] = near32(xf, yf, sxf[s], syf[s], gs, amb);
+            amb |= t0 & valid;
 #ifdef ASTRO_COLLIDE_F64
-            amb = valid;   // variant: always the exact float64 tests
+            amb = valid;   // variant: always the exact tests
 #endif
-            if (__any(amb)) {   // some lane within 1e-4 of a threshold: exact float64
+            if (__any(amb)) {   // some lane within 1e-4 of a threshold (or at tick 0): exact tests
                 bool bh64 = false, hs64[S];
 #pragma unroll
-                for (int j = 0; j < PMAX; ++j) bh64 |= (j < np) & (dist2<double>(x, y, px[j], py[j]) < p.r2_p0);
+                for (int j = 0; j < PMAX; ++j) bh64 |= (j < np) & closer_exact(x, y, px[j], py[j], gp, t0);
 #pragma unroll
-                for (int s = 0; s < S; ++s) hs64[s] = dist2<double>(x, y, sx[s], sy[s]) < p.r2_s0;
+                for (int s = 0; s < S; ++s) hs64[s] = closer_exact(x, y, sx[s], sy[s], gs, t0);
                 bh = amb ? bh64 : bh;
 #pragma unroll
                 for (int s = 0; s < S; ++s) hs[s] = amb ? hs64[s] : hs[s];
@@ -547,7 +566,7 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 bh |= hs[s];
-                hit[s] |= valid & hs[s];
+                hit[s] |= hs[s];
             }
             const C ndx = C(cur[u].z) + C(0), ndy = C(cur[u].w) + C(0);
             const C nx = C(x) + dt * ndx, ny = C(y) + dt * ndy;
@@ -559,7 +578,7 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
                 v.y = T(ny);
                 v.z = T(ndx);
                 v.w = T(ndy);
-                bullets[size_t(w) * NN + i] = v;
+                bullets[size_t(i) * BC + w] = v;
             }
             // counters as arithmetic: a conditional ++ of one of two locals
             // is folded into a store through a selected pointer, which sends
@@ -574,7 +593,7 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
 
 // New bullet of one ship (core.py:267-279) moved and culled like the others.
 template <typename C, typename T>
-__device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V *bullets, size_t NN, int i,
+__device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V *bullets, size_t BC, int i,
                                       double sx, double sy, double sdx, double sdy, float ds, float dc, int &w,
                                       int &dropped) {
     using V = typename Store<T>::V;
@@ -592,7 +611,7 @@ __device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V
         v.y = T(ny);
         v.z = T(bdx);
         v.w = T(bdy);
-        bullets[size_t(w) * NN + i] = v;
+        bullets[size_t(i) * BC + w] = v;
     }
     w += int(keep && fits);
     dropped += int(keep && !fits);
@@ -623,6 +642,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 
     if (active) {
         const size_t NN = size_t(N);
+        const size_t BC = size_t(p.b_cap);   // bullets: [N][b_cap] rows
         V *ships = reinterpret_cast<V *>(st.ships);
         T *ships_b = reinterpret_cast<T *>(st.ships_b);
         V *planets = reinterpret_cast<V *>(st.planets);
@@ -659,12 +679,13 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         const bool t0 = tick == 0;
         STAMP(1);
 
-        // ---- round 2 (needs the header): planets (padded slots re-read
-        //      slot 0), the fire word, the first bullet chunk
+        // ---- round 2: planets (every slot: padding is masked below, so
+        //      these loads do not wait for the header), the fire word, the
+        //      first bullet chunk
         double px[PMAX], py[PMAX], pdx[PMAX], pdy[PMAX];
 #pragma unroll
         for (int j = 0; j < PMAX; ++j) {
-            const int jj = j < np ? j : 0;
+            const int jj = j < p.p_pad ? j : 0;
             const V v = planets[size_t(jj) * NN + i];
             px[j] = double(v.x);
             py[j] = double(v.y);
@@ -679,7 +700,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) {
             const int k = u < nb ? u : 0;
-            buf[u] = bullets[size_t(k) * NN + i];
+            buf[u] = bullets[size_t(i) * BC + k];
         }
         n_pl = uint32_t(np);
 
@@ -717,25 +738,25 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                 bool hs = false;
 #pragma unroll
                 for (int j = 0; j < PMAX; ++j)
-                    hs |= closer32(float(sx[s]), float(sy[s]), float(px[j]), float(py[j]), gsp, t0, j < np, amb);
+                    hs |= near32(float(sx[s]), float(sy[s]), j < np ? float(px[j]) : -FAR_POS,
+                                 j < np ? float(py[j]) : -FAR_POS, gsp, amb);
                 hit[s] = hs;
             }
             bool hh = false;
-            if (S == 2)
-                hh = closer32(float(sx[0]), float(sy[0]), float(sx[S - 1]), float(sy[S - 1]), gss, t0, true, amb);
+            if (S == 2) hh = near32(float(sx[0]), float(sy[0]), float(sx[S - 1]), float(sy[S - 1]), gss, amb);
+            amb |= t0;
 #ifdef ASTRO_COLLIDE_F64
-            amb = !t0;
+            amb = true;
 #endif
-            if (__any(amb)) {   // rare: the exact float64 tests, for the ambiguous lanes
+            if (__any(amb)) {   // the exact tests, for the ambiguous and tick-0 lanes
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     bool hs = false;
 #pragma unroll
-                    for (int j = 0; j < PMAX; ++j)
-                        hs |= (j < np) & (dist2<double>(sx[s], sy[s], px[j], py[j]) < p.r2_sp);
+                    for (int j = 0; j < PMAX; ++j) hs |= (j < np) & closer_exact(sx[s], sy[s], px[j], py[j], gsp, t0);
                     hit[s] = amb ? hs : hit[s];
                 }
-                if (S == 2) hh = amb ? (dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]) < p.r2_ss) : hh;
+                if (S == 2) hh = amb ? closer_exact(sx[0], sy[0], sx[S - 1], sy[S - 1], gss, t0) : hh;
             }
             hit[0] = hit[0] || hh;
             hit[S - 1] = hit[S - 1] || hh;
@@ -745,9 +766,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         // ---- bullets
         int w = 0, dropped = 0;
         if (t0)
-            bullet_pass<float, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, true);
+            bullet_pass<float, T, S, PMAX>(p, bullets, BC, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, true);
         else
-            bullet_pass<double, T, S, PMAX>(p, bullets, NN, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, false);
+            bullet_pass<double, T, S, PMAX>(p, bullets, BC, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, false);
         n_bin = uint32_t(nb);
         STAMP(4);
 
@@ -774,9 +795,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     if (t0)
-                        spawn<float, T>(p, bullets, NN, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
+                        spawn<float, T>(p, bullets, BC, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
                     else
-                        spawn<double, T>(p, bullets, NN, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
+                        spawn<double, T>(p, bullets, BC, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
                 }
             }
 
@@ -800,10 +821,11 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             //      arrays stay float32 for the whole game)
             const float dtf = float(p.dt);
             if (np == 1) {
-                float gx, gy;
-                field<float, PMAX>(px, py, 1, px[0], py[0], p.gm, gx, gy);
-                const float ndx = float(pdx[0]) + gx * dtf;
-                const float ndy = float(pdy[0]) + gy * dtf;
+                // a lone planet's own field: r = +0, so gm / max(1e-12, 0) * r
+                // is a zero with the sign of gm, exactly
+                const float g0 = p.gm < 0.0 ? -0.0f : 0.0f;
+                const float ndx = float(pdx[0]) + g0 * dtf;
+                const float ndy = float(pdy[0]) + g0 * dtf;
                 V v;
                 v.x = T(wrap_unit<float>(float(px[0]) + dtf * ndx));
                 v.y = T(wrap_unit<float>(float(py[0]) + dtf * ndy));
@@ -939,7 +961,39 @@ __device__ __forceinline__ bool quad_any(bool f, int lane) {
     return ((__ballot(f) >> (lane & ~3)) & 0xfull) != 0;
 }
 
-constexpr int QB = 4;   // bullet rounds per prefetched chunk (16 bullets per quad)
+constexpr int QENV = BLOCK / 4;   // envs per wave in the quad kernel
+constexpr int QWIN = 1024;        // live bullets per window of the quad kernel's LDS index
+
+// Inclusive prefix sum over the 64 lanes of a wave (all lanes active): DPP
+// row shifts inside each row of 16, then the row totals.
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    const int r0 = __builtin_amdgcn_readlane(v, 15);
+    const int r1 = __builtin_amdgcn_readlane(v, 31);
+    const int r2 = __builtin_amdgcn_readlane(v, 47);
+    const int row = lane >> 4;
+    return v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
+}
+
+// Bullet index word (LDS): env in the wave | slot << 4 | last-of-env << 20 |
+// nplanets << 21 | tick-0 << 26
+__device__ __forceinline__ int bw_env(uint32_t w) { return int(w & 15u); }
+__device__ __forceinline__ int bw_slot(uint32_t w) { return int((w >> 4) & 0xffffu); }
+__device__ __forceinline__ bool bw_last(uint32_t w) { return (w >> 20) & 1u; }
+__device__ __forceinline__ int bw_np(uint32_t w) { return int((w >> 21) & 31u); }
+__device__ __forceinline__ bool bw_t0(uint32_t w) { return (w >> 26) & 1u; }
+
+// Index window [w0, w0 + QWIN) of the wave's live bullets: the quad of an
+// env whose bullets are numbered off .. off + nb - 1 writes the words of
+// those in the window, lane q taking slots k = q mod 4.
+__device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off, int nb, int q, uint32_t tag) {
+    const int lo = max(0, w0 - off), hi = min(nb, w0 + QWIN - off);
+    for (int k = lo + ((q - lo) & 3); k < hi; k += 4)
+        s_index[off + k - w0] = tag | (uint32_t(k) << 4) | (k == nb - 1 ? 1u << 20 : 0u);
+}
 
 template <typename T, int S, int PMAX>
 __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st,
@@ -949,221 +1003,293 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                                                                 unsigned long long *stats, int auto_reset) {
     using V = typename Store<T>::V;
     constexpr int PPL = PMAX / 4;   // planet slots per lane
+    constexpr int NBOD2 = (S + PMAX + 1) / 2;
+    __shared__ float4 s_body[QENV][NBOD2];              // float32 (x, y): ships, then planets (padding far)
+    __shared__ uint32_t s_index[QWIN];   // a window of the wave's live bullets, see bw_*
+    __shared__ int s_kept[QENV], s_hit[QENV];
+
     const int N = st.n_env;
     const int lane = threadIdx.x & 63;
     const int q = lane & 3;
-    const int i = (blockIdx.x * BLOCK + threadIdx.x) >> 2;
-    const bool active = i < N;   // uniform over the quad
+    const int e = lane >> 2;
+    const int base = blockIdx.x * QENV;
+    const bool active = base + e < N;     // uniform over the quad
+    const int i = active ? base + e : N - 1;   // spare quads of the last wave shadow env N-1, store nothing
+    const size_t NN = size_t(N);
+    const size_t BC = size_t(p.b_cap);
+    V *ships = reinterpret_cast<V *>(st.ships);
+    T *ships_b = reinterpret_cast<T *>(st.ships_b);
+    V *planets = reinterpret_cast<V *>(st.planets);
+    V *bullets = reinterpret_cast<V *>(st.bullets);
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
     bool f_reset = false, f_coll = false, f_tout = false;
+#ifdef ASTRO_STAMPS
+    unsigned long long stamp_[NSTAMP] = {};
+#endif
+    STAMP(0);
 
-    if (active) {
-        const size_t NN = size_t(N);
-        V *ships = reinterpret_cast<V *>(st.ships);
-        T *ships_b = reinterpret_cast<T *>(st.ships_b);
-        V *planets = reinterpret_cast<V *>(st.planets);
-        V *bullets = reinterpret_cast<V *>(st.bullets);
-
-        // ---- loads: header (every lane), own ship (lanes < S)
-        const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
-        const int sq = q < S ? q : 0;
-        const V sv = ships[size_t(sq) * NN + i];
-        const T sbv = ships_b[size_t(sq) * NN + i];
-        const int ctl = int(control[size_t(i) * S + sq]);
-        const int tick = int(uint32_t(h.x) & TICK_MASK);
-        const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
-        const uint32_t pend_seed = uint32_t(h.z);
-        int np = h.y & 0xff;
-        int flags = (h.y >> 8) & 0xff;
-        const int nb = int(uint32_t(h.y) >> 16);
-        np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
-        const bool live = tick < p.timeout_tick;
-        const bool t0 = tick == 0;
-
-        // ---- own planet slots (padded ones re-read slot 0), first bullet chunk
-        V pv[PPL];
-        T mpx[PPL], mpy[PPL];
+    // ---- loads, all independent of each other: header, own ship (lanes <
+    //      S), control, own planet slots (read whether live or not; padding
+    //      is masked below)
+    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+    const int sq = q < S ? q : 0;
+    const V sv = ships[size_t(sq) * NN + i];
+    const T sbv = ships_b[size_t(sq) * NN + i];
+    const int ctl = int(control[size_t(i) * S + sq]);
+    V pv[PPL];
+    T mpx[PPL], mpy[PPL];
 #pragma unroll
-        for (int m = 0; m < PPL; ++m) {
-            const int j = q + 4 * m;
-            pv[m] = planets[size_t(j < np ? j : 0) * NN + i];
-            mpx[m] = pv[m].x;
-            mpy[m] = pv[m].y;
+    for (int m = 0; m < PPL; ++m) {
+        const int j = q + 4 * m;
+        pv[m] = planets[size_t(j < p.p_pad ? j : 0) * NN + i];
+        mpx[m] = pv[m].x;
+        mpy[m] = pv[m].y;
+    }
+    const int tick = int(uint32_t(h.x) & TICK_MASK);
+    const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
+    const uint32_t pend_seed = uint32_t(h.z);
+    int np = h.y & 0xff;
+    const int flags = (h.y >> 8) & 0xff;
+    const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
+    np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+    const bool live = tick < p.timeout_tick;
+    const bool t0 = tick == 0;
+    STAMP(1);
+    const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
+    uint32_t pend_key = uint32_t(h.w);
+    if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
+    n_pl = active && q == 0 ? uint32_t(np) : 0u;
+
+    // ---- index the wave's live bullets densely: bullet k of env e is number
+    //      g = off_e + k, so the bullet pass below runs ceil(sum nb / 64)
+    //      rounds instead of max over envs of ceil(nb / 4)
+    const int incl = wave_incl_scan(q == 0 ? nb : 0, lane);
+    const int off = incl - nb;
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t tag = uint32_t(e) | (uint32_t(np) << 21) | (t0 ? 1u << 26 : 0u);
+    index_window(s_index, 0, off, nb, q, tag);
+    if (q == 0) {
+        s_kept[e] = 0;
+        s_hit[e] = 0;
+    }
+    __syncthreads();
+    // the first two rounds' bullets load during the physics below
+    uint32_t bw0 = lane < total ? s_index[lane] : 0u;
+    uint32_t bw1 = lane + 64 < min(total, QWIN) ? s_index[lane + 64] : 0u;
+    V cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
+    V cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
+
+    // ---- quad broadcasts: all planets, both ships
+    double px[PMAX], py[PMAX], sx[S], sy[S];
+    bcast_slots<T, 0, PPL>(mpx, px);
+    bcast_slots<T, 1, PPL>(mpx, px);
+    bcast_slots<T, 2, PPL>(mpx, px);
+    bcast_slots<T, 3, PPL>(mpx, px);
+    bcast_slots<T, 0, PPL>(mpy, py);
+    bcast_slots<T, 1, PPL>(mpy, py);
+    bcast_slots<T, 2, PPL>(mpy, py);
+    bcast_slots<T, 3, PPL>(mpy, py);
+    sx[0] = double(quad_bcast<0>(sv.x));
+    sy[0] = double(quad_bcast<0>(sv.y));
+    if (S == 2) {
+        sx[S - 1] = double(quad_bcast<S - 1>(sv.x));
+        sy[S - 1] = double(quad_bcast<S - 1>(sv.y));
+    }
+
+    // ---- own ship (lanes < S): direction, thrust + gravity (core.py:234-239)
+    const double mx = double(sv.x), my = double(sv.y), mdx = double(sv.z), mdy = double(sv.w);
+    const double mb = double(sbv);
+    float ds, dc;
+    np_sincosf(float(mb), ds, dc);
+    double ax = 0.0, ay = 0.0;
+    if (q < S) {
+        double gx, gy;
+        if (t0) {
+            float fx, fy;
+            field<float, PMAX>(px, py, np, mx, my, p.gm, fx, fy);
+            gx = double(fx);
+            gy = double(fy);
+        } else {
+            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy);
         }
-        const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
-        uint32_t pend_key = uint32_t(h.w);
-        if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
-        const int rounds = (nb + 3) >> 2;
-        V cur[QB];
+        const double thr = p.thrust * double(ctl & 1);
+        ax = thr * double(ds) + gx;
+        ay = thr * double(dc) + gy;
+    }
+
+    STAMP(2);
+    // ---- ship collisions (core.py:241-253): lane q tests its planets and
+    //      lane 0 the ship pair; quad-OR afterwards
+    const Guard gsp(p.r2_sp), gss(p.r2_ss), gp(p.r2_p0), gs(p.r2_s0);
+    float sxf[S], syf[S], mpxf[PPL], mpyf[PPL];   // float32 copies, padding parked far away
 #pragma unroll
-        for (int u = 0; u < QB; ++u) {
-            const int k = q + 4 * u;
-            cur[u] = bullets[size_t(k < nb ? k : 0) * NN + i];
-        }
-        n_pl = q == 0 ? uint32_t(np) : 0u;
-
-        // ---- quad broadcasts (uniform control flow): all planets, both ships
-        double px[PMAX], py[PMAX], sx[S], sy[S];
-        bcast_slots<T, 0, PPL>(mpx, px);
-        bcast_slots<T, 1, PPL>(mpx, px);
-        bcast_slots<T, 2, PPL>(mpx, px);
-        bcast_slots<T, 3, PPL>(mpx, px);
-        bcast_slots<T, 0, PPL>(mpy, py);
-        bcast_slots<T, 1, PPL>(mpy, py);
-        bcast_slots<T, 2, PPL>(mpy, py);
-        bcast_slots<T, 3, PPL>(mpy, py);
-        sx[0] = double(quad_bcast<0>(sv.x));
-        sy[0] = double(quad_bcast<0>(sv.y));
-        if (S == 2) {
-            sx[S - 1] = double(quad_bcast<S - 1>(sv.x));
-            sy[S - 1] = double(quad_bcast<S - 1>(sv.y));
-        }
-
-        // ---- own ship (lanes < S): direction, thrust + gravity (core.py:234-239)
-        const double mx = double(sv.x), my = double(sv.y), mdx = double(sv.z), mdy = double(sv.w);
-        const double mb = double(sbv);
-        float ds, dc;
-        np_sincosf(float(mb), ds, dc);
-        double ax = 0.0, ay = 0.0;
-        if (q < S) {
-            double gx, gy;
-            if (t0) {
-                float fx, fy;
-                field<float, PMAX>(px, py, np, mx, my, p.gm, fx, fy);
-                gx = double(fx);
-                gy = double(fy);
-            } else {
-                field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy);
-            }
-            const double thr = p.thrust * double(ctl & 1);
-            ax = thr * double(ds) + gx;
-            ay = thr * double(dc) + gy;
-        }
-
-        // ---- collisions (core.py:241-253): lane q tests its planets and its
-        //      bullets against every ship; quad-OR afterwards
-        const Guard gsp(p.r2_sp), gss(p.r2_ss), gp(p.r2_p0), gs(p.r2_s0);
-        float pxf[PMAX], pyf[PMAX], sxf[S], syf[S];
+    for (int s = 0; s < S; ++s) {
+        sxf[s] = float(sx[s]);
+        syf[s] = float(sy[s]);
+    }
 #pragma unroll
-        for (int j = 0; j < PMAX; ++j) {
-            pxf[j] = float(px[j]);
-            pyf[j] = float(py[j]);
-        }
+    for (int m = 0; m < PPL; ++m) {
+        mpxf[m] = q + 4 * m < np ? float(mpx[m]) : -FAR_POS;
+        mpyf[m] = q + 4 * m < np ? float(mpy[m]) : -FAR_POS;
+    }
+    bool hsp[S];
+    {
+        bool amb = false;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            sxf[s] = float(sx[s]);
-            syf[s] = float(sy[s]);
+            bool hs = false;
+#pragma unroll
+            for (int m = 0; m < PPL; ++m) hs |= near32(sxf[s], syf[s], mpxf[m], mpyf[m], gsp, amb);
+            hsp[s] = hs;
         }
-        bool hsp[S];
-        {
-            bool amb = false;
+        bool hh = false;
+        if (S == 2 && q == 0) hh = near32(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, amb);
+        amb |= t0;
+        if (__any(amb)) {   // the exact tests, for the ambiguous and tick-0 lanes
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 bool hs = false;
 #pragma unroll
-                for (int m = 0; m < PPL; ++m) {
-                    const int j = q + 4 * m;
-                    hs |= closer32(sxf[s], syf[s], float(mpx[m]), float(mpy[m]), gsp, t0, j < np, amb);
-                }
-                hsp[s] = hs;
+                for (int m = 0; m < PPL; ++m)
+                    hs |= (q + 4 * m < np) & closer_exact(sx[s], sy[s], double(mpx[m]), double(mpy[m]), gsp, t0);
+                hsp[s] = amb ? hs : hsp[s];
             }
-            bool hh = false;
-            if (S == 2 && q == 0) hh = closer32(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, t0, true, amb);
-            if (__any(amb)) {
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    bool hs = false;
-#pragma unroll
-                    for (int m = 0; m < PPL; ++m) {
-                        const int j = q + 4 * m;
-                        hs |= (j < np) & (dist2<double>(sx[s], sy[s], double(mpx[m]), double(mpy[m])) < p.r2_sp);
-                    }
-                    hsp[s] = amb ? hs : hsp[s];
-                }
-                if (S == 2 && q == 0) hh = amb ? (dist2<double>(sx[0], sy[0], sx[S - 1], sy[S - 1]) < p.r2_ss) : hh;
-            }
-#pragma unroll
-            for (int s = 0; s < S; ++s) hsp[s] = hsp[s] || hh;
+            if (S == 2 && q == 0) hh = amb ? closer_exact(sx[0], sy[0], sx[S - 1], sy[S - 1], gss, t0) : hh;
         }
+#pragma unroll
+        for (int s = 0; s < S; ++s) hsp[s] = hsp[s] || hh;
+    }
 
-        // ---- bullets: round r handles slots 4r..4r+3 of the quad; survivors
-        //      compacted in slot order with one ballot per round
-        int wr = 0;   // survivors so far (same in the 4 lanes), may exceed b_cap
+    // ---- old positions of the env's bodies for the bullet pass (LDS)
+    {
+        float2 *body = reinterpret_cast<float2 *>(&s_body[e][0]);
+        if (q < S) body[q] = make_float2(q == 0 ? sxf[0] : sxf[S - 1], q == 0 ? syf[0] : syf[S - 1]);
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) body[S + q + 4 * m] = make_float2(mpxf[m], mpyf[m]);
+    }
+    __syncthreads();
+
+    STAMP(3);
+    // ---- bullets (core.py:241-251, 264-266, 295-300): lane g of a round
+    //      takes live bullet r0 + g of the wave: collide with the OLD bodies,
+    //      move, cull, and compact in slot order within its env, in place
+    //      (a bullet is only ever written to a slot <= the one it was read
+    //      from, and every slot is read before any later round writes)
+    {
+        const uint64_t lanes_below = (1ull << lane) - 1;
         const double dt = p.dt;
-        bool hsb[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) hsb[s] = false;
-        const uint64_t below = (1ull << q) - 1;
-        for (int r0 = 0; r0 < rounds; r0 += QB) {
-            V nxt[QB];
-            if (r0 + QB < rounds) {
-#pragma unroll
-                for (int u = 0; u < QB; ++u) {
-                    const int k = q + 4 * (r0 + QB + u);
-                    nxt[u] = bullets[size_t(k < nb ? k : 0) * NN + i];
-                }
+        int kept_before = 0;   // kept bullets of the wave in earlier rounds
+        int carry = 0;         // kept_before at the start of the env spanning into the next round
+        for (int w0 = 0; w0 < total; w0 += QWIN) {   // uniform; one window unless > 64 bullets/env
+          const int wend = min(total, w0 + QWIN);
+          if (w0 > 0) {
+              __syncthreads();   // the previous window is read
+              index_window(s_index, w0, off, nb, q, tag);
+              __syncthreads();
+              bw0 = w0 + lane < wend ? s_index[lane] : 0u;
+              bw1 = w0 + 64 + lane < wend ? s_index[64 + lane] : 0u;
+              cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
+              cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
+          }
+          for (int r0 = w0; r0 < wend; r0 += 64) {   // uniform
+            const uint32_t bw = bw0;
+            const V cur = cur0;
+            bw0 = bw1;
+            cur0 = cur1;
+            if (r0 + 128 < wend) {   // prefetch two rounds ahead
+                bw1 = r0 + 128 + lane < wend ? s_index[r0 + 128 + lane - w0] : 0u;
+                cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
             }
+            const bool valid = r0 + lane < total;
+            const int be = bw_env(bw), bk = bw_slot(bw);
+            const bool bt0 = bw_t0(bw);
+            float bx[2 * NBOD2], by[2 * NBOD2];
 #pragma unroll
-            for (int u = 0; u < QB; ++u) {
-                if (r0 + u < rounds) {   // uniform over the quad
-                    const bool valid = q + 4 * (r0 + u) < nb;
-                    const float xf = float(cur[u].x), yf = float(cur[u].y);
-                    const double x = double(cur[u].x), y = double(cur[u].y);
-                    bool bh = false, amb = false, hs[S];
+            for (int u = 0; u < NBOD2; ++u) {
+                const float4 v = s_body[be][u];
+                bx[2 * u] = v.x;
+                by[2 * u] = v.y;
+                bx[2 * u + 1] = v.z;
+                by[2 * u + 1] = v.w;
+            }
+            const float xf = valid ? float(cur.x) : FAR_POS, yf = valid ? float(cur.y) : FAR_POS;
+            bool bh = false, amb = false, hs[S];
 #pragma unroll
-                    for (int j = 0; j < PMAX; ++j) bh |= closer32(xf, yf, pxf[j], pyf[j], gp, t0, valid & (j < np), amb);
+            for (int j = 0; j < PMAX; ++j) bh |= near32(xf, yf, bx[S + j], by[S + j], gp, amb);
 #pragma unroll
-                    for (int s = 0; s < S; ++s) hs[s] = closer32(xf, yf, sxf[s], syf[s], gs, t0, valid, amb);
-                    if (__any(amb)) {
-                        bool bh64 = false, hs64[S];
+            for (int s = 0; s < S; ++s) hs[s] = near32(xf, yf, bx[s], by[s], gs, amb);
+            amb |= valid & bt0;
+            if (__any(amb)) {
+                if (amb) {   // exact tests; the old bodies are still in memory
+                    const size_t ie = size_t(base + be);
+                    const int bnp = bw_np(bw);
+                    const double x = double(cur.x), y = double(cur.y);
+                    bool bh64 = false;
 #pragma unroll
-                        for (int j = 0; j < PMAX; ++j) bh64 |= (j < np) & (dist2<double>(x, y, px[j], py[j]) < p.r2_p0);
-#pragma unroll
-                        for (int s = 0; s < S; ++s) hs64[s] = dist2<double>(x, y, sx[s], sy[s]) < p.r2_s0;
-                        bh = amb ? bh64 : bh;
-#pragma unroll
-                        for (int s = 0; s < S; ++s) hs[s] = amb ? hs64[s] : hs[s];
+                    for (int j = 0; j < PMAX; ++j) {
+                        if (j < bnp) {
+                            const V pj = planets[size_t(j) * NN + ie];
+                            bh64 |= closer_exact(x, y, double(pj.x), double(pj.y), gp, bt0);
+                        }
                     }
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
-                        bh |= hs[s];
-                        hsb[s] |= valid & hs[s];
+                        const V sj = ships[size_t(s) * NN + ie];
+                        hs[s] = closer_exact(x, y, double(sj.x), double(sj.y), gs, bt0);
                     }
-                    bool keep;
-                    V out;
-                    if (t0) {
-                        const float dtf = float(p.dt);
-                        const float ndx = float(cur[u].z) + 0.0f, ndy = float(cur[u].w) + 0.0f;
-                        const float nx = float(x) + dtf * ndx, ny = float(y) + dtf * ndy;
-                        keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
-                        out.x = T(nx);
-                        out.y = T(ny);
-                        out.z = T(ndx);
-                        out.w = T(ndy);
-                    } else {
-                        const double ndx = double(cur[u].z) + 0.0, ndy = double(cur[u].w) + 0.0;
-                        const double nx = x + dt * ndx, ny = y + dt * ndy;
-                        keep = (-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0);
-                        out.x = T(nx);
-                        out.y = T(ny);
-                        out.z = T(ndx);
-                        out.w = T(ndy);
-                    }
-                    keep = keep & valid & !bh;
-                    const uint64_t nib = (__ballot(keep) >> (lane & ~3)) & 0xfull;
-                    const int pos = wr + __popcll(nib & below);
-                    if (keep && pos < p.b_cap) bullets[size_t(pos) * NN + i] = out;
-                    wr += __popcll(nib);
+                    bh = bh64;
                 }
             }
+            int hb = 0;
 #pragma unroll
-            for (int u = 0; u < QB; ++u) cur[u] = nxt[u];
+            for (int s = 0; s < S; ++s) {
+                bh |= hs[s];
+                hb |= hs[s] ? 1 << s : 0;
+            }
+            bool keep;
+            V out;
+            if (valid && bt0) {   // tick-0 bullets exist only in hand-made states
+                const float dtf = float(p.dt);
+                const float ndx = float(cur.z) + 0.0f, ndy = float(cur.w) + 0.0f;
+                const float nx = float(cur.x) + dtf * ndx, ny = float(cur.y) + dtf * ndy;
+                keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
+                out.x = T(nx);
+                out.y = T(ny);
+                out.z = T(ndx);
+                out.w = T(ndy);
+            } else {
+                const double ndx = double(cur.z) + 0.0, ndy = double(cur.w) + 0.0;
+                const double nx = double(cur.x) + dt * ndx, ny = double(cur.y) + dt * ndy;
+                keep = (-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0);
+                out.x = T(nx);
+                out.y = T(ny);
+                out.z = T(ndx);
+                out.w = T(ndy);
+            }
+            keep = keep & valid & !bh;
+            const uint64_t kb = __ballot(keep);
+            const int kg = kept_before + __popcll(kb & lanes_below);
+            const int first = lane - bk;   // lane of the env's slot 0 (< 0: an earlier round)
+            const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
+            const int pos = kg - k0;
+            if (keep) bullets[size_t(base + be) * BC + pos] = out;
+            if (valid && bw_last(bw)) s_kept[be] = pos + int(keep);
+            if (valid && hb) atomicOr(&s_hit[be], hb);
+            carry = __builtin_amdgcn_readlane(k0, 63);
+            kept_before += __popcll(kb);
+          }
         }
-        n_bin = q == 0 ? uint32_t(nb) : 0u;
+    }
+    __syncthreads();
+    const int wr_in = s_kept[e];
+    const int hit_bits = s_hit[e];
+    n_bin = active && q == 0 ? uint32_t(nb) : 0u;
+    STAMP(4);
 
+    if (active) {
         bool hit[S];
 #pragma unroll
-        for (int s = 0; s < S; ++s) hit[s] = quad_any(hsp[s] || hsb[s], lane);
+        for (int s = 0; s < S; ++s) hit[s] = quad_any(hsp[s], lane) || ((hit_bits >> s) & 1);
         const bool collided = S == 2 ? (hit[0] || hit[S - 1]) : hit[0];
         const bool timeout = !collided && !live;
         const uint8_t done = collided ? 1 : (timeout ? 2 : 0);
@@ -1172,9 +1298,11 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
             reward[size_t(i) * S + q] = collided ? (mh ? -1.0f : 1.0f) : (timeout ? p.timeout_reward : 0.0f);
         }
         if (q == 0) done_out[i] = done;
+        STAMP(5);
 
         if (!done) {   // uniform over the quad
             // ---- fire: ship s's bullet appended after the survivors, in ship order
+            int wr = wr_in;
             if ((fire_word >> (tick & 31)) & 1u) {
                 bool keep = false;
                 V out;
@@ -1203,8 +1331,8 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                     }
                 }
                 const uint64_t nib = (__ballot(keep) >> (lane & ~3)) & 0xfull;
-                const int pos = wr + __popcll(nib & below);
-                if (keep && pos < p.b_cap) bullets[size_t(pos) * NN + i] = out;
+                const int pos = wr + __popcll(nib & ((1ull << q) - 1));
+                if (keep && pos < p.b_cap) bullets[size_t(i) * BC + pos] = out;
                 wr += __popcll(nib);
             }
             const int w = wr < p.b_cap ? wr : p.b_cap;
@@ -1223,6 +1351,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                 ships_b[size_t(q) * NN + i] = T(mb + p.db * double((ctl >> 1) - 1));
             }
 
+            STAMP(6);
             // ---- own planets: gravity of all planets incl. self, in order
             //      (core.py:289-294); float32 at tick 0 / for a lone planet
             const float dtf = float(p.dt);
@@ -1234,9 +1363,10 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                     const double pdx = double(pv[m].z), pdy = double(pv[m].w);
                     V v;
                     if (np == 1) {
-                        float gx, gy;
-                        field<float, PMAX>(px, py, 1, pxj, pyj, p.gm, gx, gy);
-                        const float ndx = float(pdx) + gx * dtf, ndy = float(pdy) + gy * dtf;
+                        // a lone planet's own field: r = +0, so gm / max(1e-12, 0) * r
+                        // is a zero with the sign of gm, exactly
+                        const float g0 = p.gm < 0.0 ? -0.0f : 0.0f;
+                        const float ndx = float(pdx) + g0 * dtf, ndy = float(pdy) + g0 * dtf;
                         v.x = T(wrap_unit<float>(float(pxj) + dtf * ndx));
                         v.y = T(wrap_unit<float>(float(pyj) + dtf * ndy));
                         v.z = T(ndx);
@@ -1263,6 +1393,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                 }
             }
 
+            STAMP(7);
             if (q == 0) {
                 const int fl = flags | (dropped ? 1 : 0);
                 const uint32_t kv = (key_valid || p.key_table) ? KEY_VALID : 0u;
@@ -1271,15 +1402,27 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                 n_bout = uint32_t(w);
                 n_drop = uint32_t(dropped);
             }
-        } else if (q == 0) {
-            f_coll = collided;
-            f_tout = timeout;
-            if (auto_reset) {
-                restart_from_stream<T, S, PMAX>(p, st, i, pend_seed, pend_key, key_valid || p.key_table);
-                f_reset = true;
+            STAMP(8);
+        } else {
+            STAMP(9);
+            f_coll = q == 0 && collided;
+            f_tout = q == 0 && timeout;
+            if (auto_reset) {   // the whole quad creates the next game
+                const uint32_t key = uint32_t(quad_bcast_i<0>(int(pend_key)));   // lane q == 0 fetched it
+                restart_from_stream<T, S, PMAX, 4>(p, st, i, pend_seed, key, key_valid || p.key_table, q);
+                f_reset = q == 0;
             }
+            STAMP(10);
         }
     }
+    STAMP(11);
+#ifdef ASTRO_STAMPS
+    if (stats && lane == 0) {
+        unsigned long long *row = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * NSTAMP;
+        for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
+    }
+    return;
+#endif
 
     if (stats) {   // one private row per wave (16 envs)
         const uint64_t m_reset = __ballot(f_reset), m_coll = __ballot(f_coll), m_tout = __ballot(f_tout);

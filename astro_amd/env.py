@@ -10,10 +10,12 @@ tick and, for games that end, starts the env's next game in the same kernel
 (core.py:77-83), indexed by GLOBAL env id, so a run sharded over G GPUs
 (``env_offset``) plays exactly the games of a 1-GPU run.
 
-All state lives in HBM as PyTorch tensors, struct-of-arrays, entity-major:
+All state lives in HBM as PyTorch tensors; ships and planets struct-of-arrays,
+entity-major (a wave's lanes read contiguous rows), bullets one contiguous row
+per env (the kernels walk an env's live bullets in slot order):
 
     ships    [S, N, 4]   x, y, dx, dy        ships_b  [S, N]
-    planets  [P, N, 4]   x, y, dx, dy        bullets  [B, N, 4]
+    planets  [P, N, 4]   x, y, dx, dy        bullets  [N, B, 4]
     hdr      [N, 4]      tick | chain << 22, nplanets | flags << 8 | nbullets << 16,
                          next game's init-chain value, next game's seed
     stream   [N, 4]      seed-stream cursor + current game's seed
@@ -105,7 +107,7 @@ class BatchedEnv:
         self.ships = z(S, N, 4)
         self.ships_b = z(S, N)
         self.planets = z(self.p_pad, N, 4)
-        self.bullets = z(self.b_cap, N, 4)
+        self.bullets = z(N, self.b_cap, 4)
         self.hdr = z(N, 4, dt=torch.int32)
         self.stream = z(N, 4, dt=torch.int32)
         self.reward = z(N, S, dt=torch.float32)
@@ -205,7 +207,7 @@ class BatchedEnv:
         return Observation(
             ships=self.ships.permute(1, 0, 2), ships_b=self.ships_b.permute(1, 0),
             planets=self.planets.permute(1, 0, 2), nplanets=self.nplanets,
-            bullets=self.bullets.permute(1, 0, 2), nbullets=self.nbullets, tick=self.tick)
+            bullets=self.bullets, nbullets=self.nbullets, tick=self.tick)
 
     def stat_dict(self):
         v = self.stats.sum(0).cpu().tolist()
@@ -218,7 +220,7 @@ class BatchedEnv:
         return dict(ships=self.ships.permute(1, 0, 2).cpu().numpy(),
                     ships_b=self.ships_b.permute(1, 0).cpu().numpy(),
                     planets=self.planets.permute(1, 0, 2).cpu().numpy(),
-                    bullets=self.bullets.permute(1, 0, 2).cpu().numpy(),
+                    bullets=self.bullets.cpu().numpy(),
                     tick=self.tick.cpu().numpy(), nplanets=self.nplanets.cpu().numpy(),
                     nbullets=self.nbullets.cpu().numpy(), flags=self.flags.cpu().numpy())
 
@@ -237,7 +239,7 @@ class BatchedEnv:
         bsrc = np.asarray(bullets)
         nbmax = min(bsrc.shape[1], self.b_cap)
         bl[:, :nbmax] = bsrc[:, :nbmax]
-        put(self.bullets, bl.transpose(1, 0, 2))
+        put(self.bullets, bl)
         nb = np.asarray(nbullets, dtype=np.int64)
         if (nb > self.b_cap).any():
             raise ValueError('a state holds more bullets than b_cap')

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 4
+#define ASTRO_ABI_VERSION 5
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -70,8 +70,10 @@ typedef struct AstroParams {
 } AstroParams;
 
 /* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:
- * four lanes per env (16 envs per wave), for batches too small to give each
- * SIMD several waves.  AUTO picks QUAD for n_env <= ASTRO_QUAD_MAX_ENVS. */
+ * four lanes per env (16 envs per wave) for ships and planets, and the wave's
+ * live bullets spread densely over its 64 lanes; for batches too small to
+ * give each SIMD several waves.  AUTO picks QUAD for n_env <=
+ * ASTRO_QUAD_MAX_ENVS.  Both give identical results. */
 enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2 };
 #define ASTRO_QUAD_MAX_ENVS 65536
 
@@ -88,7 +90,7 @@ typedef struct AstroState {
     void *ships;        /* [nships][n_env][4]  x, y, dx, dy */
     void *ships_b;      /* [nships][n_env]     bearing */
     void *planets;      /* [p_pad][n_env][4]   x, y, dx, dy */
-    void *bullets;      /* [b_cap][n_env][4]   x, y, dx, dy */
+    void *bullets;      /* [n_env][b_cap][4]   x, y, dx, dy (one contiguous row per env) */
     int32_t *hdr;       /* [n_env][4], 16-byte aligned */
     uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, current game's seed */
     int32_t n_env;

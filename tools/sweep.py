@@ -53,13 +53,14 @@ def use_lib(name):
     _lib.load(os.path.join(ROOT, 'astro_amd', name))
 
 
-def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hip_stamps.so'):
+def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hip_stamps.so',
+           kernel='lane'):
     """Per-section cycle shares from the -DASTRO_STAMPS diagnostic library."""
     from astro_amd import _lib
     use_lib(lib)
-    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad)
+    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, kernel=kernel)
     env.reset()
-    nw = (n + 63) // 64
+    nw = (n + 63) // 64 if kernel == 'lane' else (n + 15) // 16
     env.stats = torch.zeros(nw, 16, dtype=torch.int64, device='cuda')
     ctl = torch.from_numpy(bench.controls(0, n, env.S, warm + ticks)).cuda()
     for t in range(warm):
@@ -82,7 +83,13 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
                             chain_hdr=(7, 8), reset=(9, 10)).items():
         out[key] = seg(a, b)
     out['branches_total'] = float((S[:, 11] - S[:, 5]).mean())
-    out['start_skew'] = float(s0.max() - s0.min())
+    slow = tot >= np.percentile(tot, 90)
+    Sm = S[slow]
+    for key, (a, b) in dict(hdr_wait=(0, 1), loads2_sincos_gravity=(1, 2), ship_collide=(2, 3),
+                            bullets=(3, 4), reward=(4, 5), branches=(5, 11)).items():
+        out['slow10_' + key] = float((Sm[:, b] - Sm[:, a]).mean())
+    out['slow10_total'] = float(tot[slow].mean())
+    out['slow10_reset_share'] = float(((Sm[:, 9] > 0) & (Sm[:, 10] > 0)).mean())
     print(json.dumps(out), flush=True)
     _lib._lib = None
 
@@ -151,6 +158,8 @@ def main():
             stamps(lib + ':c3', D, 65536, lib=lib + '_stamps.so')
         return
     if a.set == 'stamps':
+        stamps('quad_c3', D, 65536, kernel='quad')
+        stamps('quad_c2', D._replace(reload_time=1000), 65536, kernel='quad')
         stamps('c3', D, 65536)
         stamps('c2', D._replace(reload_time=1000), 65536)
         stamps('c3_16k', D, 16384)
