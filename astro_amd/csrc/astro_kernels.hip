@@ -332,13 +332,93 @@ constexpr double TWO_PI = 6.283185307179586;  // 2 * np.pi
 constexpr double PI = 3.141592653589793;      // np.pi
 
 // ---------------------------------------------------------------------------
+// The random draws of create() (core.py:88-116), in the reference's order:
+// randint(1, max_planets + 1), rand(2) (outer), rand() (inner), rand() (ship
+// choice, only with > 1 planet), rand(S) (bearings), then with > 1 planet
+// rand() (orientation) and choice((-1, 1)) = randint(0, 2).
+
+template <int S>
+struct CreateDraws {
+    int n;
+    double u_out[2], u_inner, u_choice, u_bear[S], u_base;
+    int reverse;
+    bool exhausted;   // the seed's first 227 outputs did not suffice
+};
+
+__device__ __forceinline__ double rand53(uint32_t hi, uint32_t lo) {   // RandomState.rand() of two words
+    return (double(hi >> 5) * 67108864.0 + double(lo >> 6)) / 9007199254740992.0;
+}
+
+// The integer half of create(): randint(1, max_planets + 1) draws whole
+// words until one passes the mask (once, for max_planets a power of two);
+// every later draw sits at a fixed offset from the accepted word given
+// n > 1 or not, so the remaining 11 + 2S words are produced straight-line.
+// Called with uniform arguments (one env at a time, see next_game_scalar)
+// this all runs on the scalar unit.
+template <int S>
+struct CreateWords {
+    static constexpr int CW = 11 + 2 * S;
+    int n;
+    uint32_t w[CW];
+    bool exhausted;   // the seed's first 227 words did not suffice
+};
+
+template <int S>
+__device__ __forceinline__ CreateWords<S> create_words(const AstroParams &p, uint32_t seed, uint32_t key397) {
+    constexpr int CW = CreateWords<S>::CW;
+    CreateWords<S> cw;
+    MTLazy g;
+    g.seed_from(seed, key397);
+    cw.n = g.randint(1, p.max_planets + 1);
+    uint32_t a = g.a, b = g.b;
+    const uint32_t i0 = g.i;
+#pragma unroll
+    for (int k = 0; k < CW; ++k) {
+        const uint32_t a1 = mt_key_next(a, i0 + uint32_t(k + 1));
+        const uint32_t y = (a & 0x80000000u) | (a1 & 0x7fffffffu);
+        const uint32_t tw = b ^ (y >> 1) ^ ((a1 & 1u) ? 0x9908b0dfu : 0u);
+        b = mt_key_next(b, i0 + uint32_t(k + 398));
+        a = a1;
+        cw.w[k] = mt_temper(tw);
+    }
+    const uint32_t used = i0 + uint32_t(cw.n > 1 ? CW : 6 + 2 * S);
+    cw.exhausted = used >= 227u || !g.ok();   // MTLazy: valid for the first 227 words
+    return cw;
+}
+
+// The float half: the draws as RandomState.rand() values.  (Both word
+// layouts are converted and the results selected: selecting between array
+// elements would index the array in memory.)
+template <int S>
+__device__ __forceinline__ CreateDraws<S> create_draws(const CreateWords<S> &cw) {
+    const uint32_t *w = cw.w;
+    CreateDraws<S> d;
+    d.n = cw.n;
+    const bool many = d.n > 1;
+    d.u_out[0] = rand53(w[0], w[1]);
+    d.u_out[1] = rand53(w[2], w[3]);
+    d.u_inner = rand53(w[4], w[5]);
+    d.u_choice = many ? rand53(w[6], w[7]) : 1.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const double u_many = rand53(w[8 + 2 * s], w[9 + 2 * s]);
+        const double u_one = rand53(w[6 + 2 * s], w[7 + 2 * s]);
+        d.u_bear[s] = many ? u_many : u_one;
+    }
+    d.u_base = many ? rand53(w[8 + 2 * S], w[9 + 2 * S]) : 0.0;
+    d.reverse = many && (w[10 + 2 * S] & 1u) == 0 ? -1 : 1;   // choice((-1, 1)) = randint(0, 2)
+    d.exhausted = cw.exhausted;
+    return d;
+}
+
+// ---------------------------------------------------------------------------
 // create() (core.py:86-135) for env i from `seed`; writes the env's slots.
 // NPART lanes may share one env: each runs the (cheap, serial) random draws
 // and writes ships s and planets j with s, j = part mod NPART, so the
 // trigonometry of the planets runs in parallel.
 
 template <typename T, int S, int PMAX, int NPART = 1>
-__device__ int create_env(const AstroParams &p, const AstroState &st, int i, uint32_t seed, uint32_t key397,
+__device__ int create_env(const AstroParams &p, const AstroState &st, int i, const CreateDraws<S> &d,
                           int &flags_out, int part = 0) {
     using V = typename Store<T>::V;
     const size_t N = size_t(st.n_env);
@@ -359,35 +439,32 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
             planets[size_t(j) * N + i] = w;
         }
         flags_out = 0;
-        (void)seed; (void)key397;
+        (void)d;
         return PMAX < 3 ? PMAX : 3;
     }
 #endif
-    MTLazy g;
-    g.seed_from(seed, key397);
-    int n = g.randint(1, p.max_planets + 1);
+    int n = d.n;
     // outer = outer_ship_position * sign(rand(2).astype(float32) - 0.5)
-    const float u0 = float(g.rand()) - 0.5f;
-    const float u1 = float(g.rand()) - 0.5f;
+    const float u0 = float(d.u_out[0]) - 0.5f;
+    const float u1 = float(d.u_out[1]) - 0.5f;
     const float o0 = p.outer_pos * (u0 > 0.0f ? 1.0f : (u0 < 0.0f ? -1.0f : 0.0f));
     const float o1 = p.outer_pos * (u1 > 0.0f ? 1.0f : (u1 < 0.0f ? -1.0f : 0.0f));
     // inner = inner_ship_position * direction(2 pi rand())
     float is, ic;
-    np_sincosf(float(TWO_PI * g.rand()), is, ic);
+    np_sincosf(float(TWO_PI * d.u_inner), is, ic);
     const float i0 = p.inner_pos * is, i1 = p.inner_pos * ic;
     float shx[2], shy[2];
+    const bool outer_first = d.u_choice < 0.5;
     if (n == 1) {
         shx[0] = o0;
         shy[0] = o1;
         shx[1] = -o0;
         shy[1] = -o1;
     } else if (S == 1) {
-        const bool outer = g.rand() < 0.5;
-        shx[0] = outer ? o0 : i0;
-        shy[0] = outer ? o1 : i1;
+        shx[0] = outer_first ? o0 : i0;
+        shy[0] = outer_first ? o1 : i1;
         shx[1] = shy[1] = 0.0f;
     } else {
-        const bool outer_first = g.rand() < 0.5;
         shx[0] = outer_first ? o0 : i0;
         shy[0] = outer_first ? o1 : i1;
         shx[1] = outer_first ? i0 : o0;
@@ -396,7 +473,7 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
     // b = 2 pi * rand(S).astype(float32)   (float32 product)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        const float b = 6.2831855f * float(g.rand());
+        const float b = 6.2831855f * float(d.u_bear[s]);
         V v;
         v.x = T(shx[s]);
         v.y = T(shy[s]);
@@ -412,15 +489,15 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
         v.x = v.y = v.z = v.w = T(0);
         if (part == 0) planets[i] = v;
     } else {
-        const double base = TWO_PI * g.rand();
+        const double base = TWO_PI * d.u_base;
         const double stp = TWO_PI / double(n);
-        const int reverse = g.randint(0, 2) == 0 ? -1 : 1;
+        const int reverse = d.reverse;
         const double amp = sqrt(p.gravity * p.planet_mass * double(n - 1) / 2.0);
         const double turn = double(reverse) * PI / 2.0;
 #pragma unroll
-        for (int m = 0; m < PMAX / NPART; ++m) {
+        for (int m = 0; m < (PMAX + NPART - 1) / NPART; ++m) {
             const int j = part + NPART * m;
-            if (j >= n) continue;
+            if (j >= n || j >= PMAX) continue;
             const double orient = base + double(j) * stp;
             float ps, pc, vs, vc;
             np_sincosf(float(orient), ps, pc);
@@ -434,7 +511,7 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
         }
     }
     if (n > PMAX) n = PMAX;
-    flags_out = g.ok() ? 0 : 2;
+    flags_out = d.exhausted ? 2 : 0;
     return n;
 }
 
@@ -449,24 +526,45 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, uin
 // key[397] of that seed fetched from the key table by an earlier step (hdr
 // word 3, valid when KEY_VALID); create, then draw the following seed.  The
 // following seed's key is gathered by the NEXT step, off this path.
-template <typename T, int S, int PMAX, int NPART = 1>
-__device__ __forceinline__ void restart_from_stream(const AstroParams &p, const AstroState &st, int i,
-                                                    uint32_t pend_seed, uint32_t pend_key, bool key_valid,
-                                                    int part = 0) {
-    uint4 c = reinterpret_cast<uint4 *>(st.stream)[i];   // in flight during create
-    const uint32_t key397 = key_valid ? pend_key : key397_of(p, pend_seed);
-    int cf = 0;
-    const int n = create_env<T, S, PMAX, NPART>(p, st, i, pend_seed, key397, cf, part);
-    if (part != 0) return;
+// Everything integer about an env's next game: the create() words of its
+// pending seed and the stream cursor advanced by one game (core.py:83).
+template <int S>
+struct NextGame {
+    CreateWords<S> words;
+    uint32_t ca, cb, ci;   // advanced cursor
+    uint32_t next_seed;    // the game after
+    bool exhausted;
+};
+
+// (key397 of the pending seed is either known or, have_key false, run here)
+template <int S>
+__device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t pend_seed, uint32_t key397,
+                                                 bool have_key, uint32_t ca, uint32_t cb, uint32_t ci) {
+    NextGame<S> ng;
+    ng.words = create_words<S>(p, pend_seed, have_key ? key397 : mt_key_at(pend_seed, 0, MT_PROLOGUE));
     MTLazy g;
-    g.a = c.x;
-    g.b = c.y;
-    g.i = c.z;
-    const bool exhausted = !g.ok();
-    const uint32_t next_seed = g.next() & SEED_MASK;
-    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, pend_seed);
-    const int flags = (exhausted || cf) ? 2 : 0;
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(next_seed), 0);
+    g.a = ca;
+    g.b = cb;
+    g.i = ci;
+    ng.exhausted = !g.ok() || ng.words.exhausted;
+    ng.next_seed = g.next() & SEED_MASK;
+    ng.ca = g.a;
+    ng.cb = g.b;
+    ng.ci = g.i;
+    return ng;
+}
+
+// Start env i's next game from its NextGame: create (the float half), then
+// the stream record and header (part 0).
+template <typename T, int S, int PMAX, int NPART = 1>
+__device__ __forceinline__ void restart_env(const AstroParams &p, const AstroState &st, int i, uint32_t pend_seed,
+                                            const NextGame<S> &ng, int part = 0) {
+    int cf = 0;
+    const int n = create_env<T, S, PMAX, NPART>(p, st, i, create_draws<S>(ng.words), cf, part);
+    if (part != 0) return;
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(ng.ca, ng.cb, ng.ci, pend_seed);
+    const int flags = (ng.exhausted || cf) ? 2 : 0;
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(ng.next_seed), 0);
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -489,6 +587,10 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
         __builtin_amdgcn_sched_barrier(0);                                               \
         stamp_[k] = t_;                                                                  \
+        if (k == 0 || k == 11) {   /* 100 MHz wall clock too: shader clock = ratio */      \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+            stamp_[k == 0 ? 12 : 13] = t_;                                                \
+        }                                                                                \
     } while (0)
 constexpr int NSTAMP = 16;
 #else
@@ -877,7 +979,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             f_coll = collided;
             f_tout = timeout;
             if (auto_reset) {
-                restart_from_stream<T, S, PMAX>(p, st, i, pend_seed, pend_key, key_valid || p.key_table);
+                const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+                const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, c.x, c.y, c.z);
+                restart_env<T, S, PMAX>(p, st, i, pend_seed, ng);
                 f_reset = true;
             }
             STAMP(10);
@@ -995,6 +1099,105 @@ __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off,
         s_index[off + k - w0] = tag | (uint32_t(k) << 4) | (k == nb - 1 ? 1u << 20 : 0u);
 }
 
+// One pass of the quad kernel's auto-reset: the next game (core.py:83,
+// 86-135) of up to four finished envs at once, 16 lanes per env (row r of
+// the wave serves the r-th lowest leader lane in `todo`).  create()'s draws
+// are the first 12 + 2S outputs of RandomState(seed) when randint(1,
+// max_planets + 1) accepts its first word: lane u of the row yields output
+// u, its two init-key inputs coming from the row's lanes 0 (seed chain) and
+// 1 (key[397] chain) through LDS, so the serial part is one chain step per
+// output instead of two chains plus tempering; the float work of create()
+// then runs spread over the row (ship u, planet u).  An env whose first
+// randint word is rejected is flagged in s_serial for the quad's serial
+// create.  Returns the leaders not yet served.
+template <typename T, int S, int PMAX>
+__device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
+                                                    int lane, int i, uint32_t pend_seed, uint32_t pend_key,
+                                                    bool have_key, uint32_t (*s_chain)[2][13 + 2 * S],
+                                                    int *s_serial) {
+    constexpr int NW = 12 + 2 * S;   // outputs create() draws, randint accepting its first word
+    int leader[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // uniform
+        leader[r] = todo ? int(__builtin_ctzll(todo)) : -1;
+        todo &= todo ? todo - 1 : 0;
+    }
+    const int row = lane >> 4, u = lane & 15, row0 = lane & ~15;
+    const int L = row == 0 ? leader[0] : row == 1 ? leader[1] : row == 2 ? leader[2] : leader[3];
+    const bool on = L >= 0;
+    const int src = on ? L : 0;
+    const int ie = __shfl(i, src, 64);
+    const uint32_t seed = uint32_t(__shfl(int(pend_seed), src, 64));
+    const uint32_t key = uint32_t(__shfl(int(pend_key), src, 64));
+    const bool hk = __shfl(int(have_key), src, 64) != 0;
+    const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[ie];   // used last: in flight meanwhile
+
+    // init-key chains: even lanes run key[0..] from the seed, odd lanes key[397..]
+    const uint32_t k397 = hk ? key : mt_key_at(seed, 0, MT_PROLOGUE);
+    const bool bchain = u & 1;
+    uint32_t x = bchain ? k397 : seed;
+    const uint32_t koff = bchain ? 397u : 0u;
+    if (u < 2) s_chain[row][u][0] = x;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        x = mt_key_next(x, koff + uint32_t(k + 1));
+        if (u < 2) s_chain[row][u][k + 1] = x;
+    }
+    __syncthreads();
+    const int uw = u < NW ? u : 0;
+    const uint32_t a0 = s_chain[row][0][uw], a1 = s_chain[row][0][uw + 1], b0 = s_chain[row][1][uw];
+    __syncthreads();   // s_chain is free for the next pass
+    const uint32_t y = (a0 & 0x80000000u) | (a1 & 0x7fffffffu);
+    const uint32_t w = mt_temper(b0 ^ (y >> 1) ^ ((a1 & 1u) ? 0x9908b0dfu : 0u));   // output u
+
+    // randint(1, max_planets + 1) on output 0
+    const uint32_t rng = uint32_t(p.max_planets - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    const uint32_t v = uint32_t(__shfl(int(w), row0, 64)) & mask;
+    const bool fast = rng != 0 && v <= rng;
+    // lane k of the row: R_k = rand() of outputs k, k + 1
+    const uint32_t wn = uint32_t(__shfl(int(w), row0 | ((u + 1) & 15), 64));
+    const double R = rand53(w, wn);
+    CreateDraws<S> d;
+    d.n = 1 + int(v);
+    const bool many = d.n > 1;
+    d.u_out[0] = __shfl(R, row0 | 1, 64);
+    d.u_out[1] = __shfl(R, row0 | 3, 64);
+    d.u_inner = __shfl(R, row0 | 5, 64);
+    // (every shuffle unconditional: its source lane must be active)
+    const double r_choice = __shfl(R, row0 | 7, 64);
+    const double r_base = __shfl(R, row0 | (9 + 2 * S), 64);
+    const uint32_t w_rev = uint32_t(__shfl(int(w), row0 | (11 + 2 * S), 64));
+    d.u_choice = many ? r_choice : 1.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) d.u_bear[s] = __shfl(R, row0 | ((many ? 9 : 7) + 2 * s), 64);
+    d.u_base = many ? r_base : 0.0;
+    d.reverse = many && (w_rev & 1u) == 0 ? -1 : 1;
+    d.exhausted = false;   // NW outputs, far below the 227 the lazy generator covers
+
+    if (on && fast) {
+        int cf = 0;
+        const int n = create_env<T, S, PMAX, 16>(p, st, ie, d, cf, u);
+        if (u == 0) {   // the stream record and header, as restart_env
+            MTLazy g;
+            g.a = c.x;
+            g.b = c.y;
+            g.i = c.z;
+            const bool exhausted = !g.ok();
+            const uint32_t next_seed = g.next() & SEED_MASK;
+            reinterpret_cast<uint4 *>(st.stream)[ie] = make_uint4(g.a, g.b, g.i, seed);
+            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | ((exhausted || cf) ? 2 << 8 : 0), int(next_seed), 0);
+        }
+    }
+    if (on && !fast && u == 0) s_serial[L >> 2] = 1;
+    return todo;
+}
+
 template <typename T, int S, int PMAX>
 __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st,
                                                                 const int8_t *__restrict__ control,
@@ -1006,7 +1209,8 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
     __shared__ float4 s_body[QENV][NBOD2];              // float32 (x, y): ships, then planets (padding far)
     __shared__ uint32_t s_index[QWIN];   // a window of the wave's live bullets, see bw_*
-    __shared__ int s_kept[QENV], s_hit[QENV];
+    __shared__ int s_kept[QENV], s_hit[QENV], s_serial[QENV];
+    __shared__ uint32_t s_chain[4][2][13 + 2 * S];      // init-key chains of a reset pass, see below
 
     const int N = st.n_env;
     const int lane = threadIdx.x & 63;
@@ -1023,6 +1227,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     V *bullets = reinterpret_cast<V *>(st.bullets);
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
     bool f_reset = false, f_coll = false, f_tout = false;
+    bool need_reset = false;   // leader lane (q == 0) of an env whose game ended, auto-reset on
 #ifdef ASTRO_STAMPS
     unsigned long long stamp_[NSTAMP] = {};
 #endif
@@ -1071,6 +1276,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     if (q == 0) {
         s_kept[e] = 0;
         s_hit[e] = 0;
+        s_serial[e] = 0;
     }
     __syncthreads();
     // the first two rounds' bullets load during the physics below
@@ -1407,14 +1613,27 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
             STAMP(9);
             f_coll = q == 0 && collided;
             f_tout = q == 0 && timeout;
-            if (auto_reset) {   // the whole quad creates the next game
-                const uint32_t key = uint32_t(quad_bcast_i<0>(int(pend_key)));   // lane q == 0 fetched it
-                restart_from_stream<T, S, PMAX, 4>(p, st, i, pend_seed, key, key_valid || p.key_table, q);
-                f_reset = q == 0;
-            }
-            STAMP(10);
+            need_reset = auto_reset && q == 0;
+            f_reset = need_reset;
         }
     }
+
+    // ---- auto-reset: the wave creates its finished envs' next games together,
+    //      up to four per pass with 16 lanes each (wave_reset_pass); rejected
+    //      randint words (max_planets not a power of two) take the serial path
+    for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
+        todo = wave_reset_pass<T, S, PMAX>(p, st, todo, lane, i, pend_seed, pend_key, key_valid || p.key_table,
+                                           s_chain, s_serial);
+    if (auto_reset) {
+        __syncthreads();
+        if (active && s_serial[e]) {   // uniform over the quad; rare
+            const uint32_t kq = uint32_t(quad_bcast_i<0>(int(pend_key)));   // lane q == 0 fetched it
+            const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+            const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, c.x, c.y, c.z);
+            restart_env<T, S, PMAX, 4>(p, st, i, pend_seed, ng, q);
+        }
+    }
+    STAMP(10);
     STAMP(11);
 #ifdef ASTRO_STAMPS
     if (stats && lane == 0) {
@@ -1456,13 +1675,16 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
     if (mask && !mask[i]) return;
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
     if (!seeds) {
-        restart_from_stream<T, S, PMAX>(p, st, i, uint32_t(h.z), uint32_t(h.w), (uint32_t(h.x) & KEY_VALID) != 0);
+        const uint32_t seed = uint32_t(h.z);
+        const uint32_t key = (uint32_t(h.x) & KEY_VALID) ? uint32_t(h.w) : key397_of(p, seed);
+        const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+        restart_env<T, S, PMAX>(p, st, i, seed, next_game<S>(p, seed, key, true, c.x, c.y, c.z));
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued
     int cf = 0;
     const uint32_t seed = seeds[i];
-    const int n = create_env<T, S, PMAX>(p, st, i, seed, key397_of(p, seed), cf);
+    const int n = create_env<T, S, PMAX>(p, st, i, create_draws<S>(create_words<S>(p, seed, key397_of(p, seed))), cf);
     reinterpret_cast<int4 *>(st.hdr)[i] =
         make_int4(int(uint32_t(h.x) & ~TICK_MASK), n | ((cf ? 2 : 0) << 8), h.z, h.w);
     if (st.stream) reinterpret_cast<uint32_t *>(st.stream)[4 * i + 3] = seed;

@@ -89,6 +89,10 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
                             bullets=(3, 4), reward=(4, 5), branches=(5, 11)).items():
         out['slow10_' + key] = float((Sm[:, b] - Sm[:, a]).mean())
     out['slow10_total'] = float(tot[slow].mean())
+    rt = (S[:, 13] - S[:, 12]).astype(np.float64)
+    out['sclk_mhz'] = float((tot / np.maximum(rt, 1)).mean() * 100.0)
+    out['wave_us_max'] = float(rt.max() / 100.0)
+    out['wave_us_mean'] = float(rt.mean() / 100.0)
     out['slow10_reset_share'] = float(((Sm[:, 9] > 0) & (Sm[:, 10] > 0)).mean())
     print(json.dumps(out), flush=True)
     _lib._lib = None
