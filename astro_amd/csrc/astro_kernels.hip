@@ -1636,6 +1636,15 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     STAMP(10);
     STAMP(11);
 #ifdef ASTRO_STAMPS
+    {   // where the wave ran and what it carried: per-SIMD load attribution
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const unsigned long long n_res = __popcll(__ballot(f_reset));
+        const unsigned long long n_t0 = __popcll(__ballot(active && q == 0 && t0));
+        stamp_[14] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        stamp_[15] = n_res | (n_t0 << 8) | ((unsigned long long)total << 16);
+    }
     if (stats && lane == 0) {
         unsigned long long *row = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * NSTAMP;
         for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];

@@ -61,7 +61,8 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
     env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, kernel=kernel)
     env.reset()
     nw = (n + 63) // 64 if kernel == 'lane' else (n + 15) // 16
-    env.stats = torch.zeros(nw, 16, dtype=torch.int64, device='cuda')
+    ncr = 0
+    env.stats = torch.zeros(nw + ncr, 16, dtype=torch.int64, device='cuda')
     ctl = torch.from_numpy(bench.controls(0, n, env.S, warm + ticks)).cuda()
     for t in range(warm):
         env.launch(ctl[t].data_ptr(), stats=False)
@@ -71,7 +72,9 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
         env.launch(ctl[warm + t].data_ptr(), stats=True)
         torch.cuda.synchronize()
         rows.append(env.stats.cpu().numpy().astype(np.int64))
-    S = np.concatenate(rows, 0)
+    R = np.stack(rows, 0)            # [ticks, nw + ncr, 16]
+    C = R[:, nw:, :]                 # creator rows
+    S = R[:, :nw, :].reshape(-1, 16)
     s0 = S[:, 0]
     tot = S[:, 11] - s0
     out = dict(name=name, n=n, wave_cycles_mean=float(tot.mean()), wave_cycles_max=float(tot.max()))
@@ -93,6 +96,52 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
     out['sclk_mhz'] = float((tot / np.maximum(rt, 1)).mean() * 100.0)
     out['wave_us_max'] = float(rt.max() / 100.0)
     out['wave_us_mean'] = float(rt.mean() / 100.0)
+    if ncr:
+        t0 = R[:, :nw, 12].min(1)[:, None].astype(np.float64)
+        cs, cl, ce = [(C[:, :, k] - t0) / 100.0 for k in (0, 1, 2)]
+        step_end = ((R[:, :nw, 13] - t0) / 100.0)
+        out['creator_us'] = dict(start_mean=float(cs.mean()), start_max=float(cs.max()),
+                                 last_flag_mean=float(cl.mean()), last_flag_max=float(cl.max()),
+                                 end_mean=float(ce.mean()), end_max=float(ce.max()),
+                                 step_end_max=float(step_end.max(1).mean()),
+                                 served_mean=float(C[:, :, 3].mean()), batches_mean=float(C[:, :, 4].mean()))
+        # publish (step wave slot 10) -> seen (creator slots 5..12) delay
+        pub = R[:, :nw, 10].astype(np.float64)
+        seen = C[:, :, 5:13].reshape(C.shape[0], -1)[:, :nw].astype(np.float64)
+        ok = (pub > 0) & (seen > 0)
+        dly = (seen - pub)[ok] / 100.0
+        out['flag_delay_us'] = dict(mean=float(dly.mean()), p99=float(np.percentile(dly, 99)), max=float(dly.max()))
+        pubrel = ((pub - t0) / 100.0)[ok]
+        out['publish_us'] = dict(mean=float(pubrel.mean()), max=float(pubrel.max()))
+    if kernel == 'quad':   # per-SIMD attribution (slots 14, 15 of the quad kernel's stamps)
+        hw = S[:, 14] & 0xffffffff
+        simd = ((S[:, 14] >> 32) << 16) | ((hw >> 4) & 0xfff)   # xcc | se, sh, cu, simd
+        res, t0n, bul = S[:, 15] & 0xff, (S[:, 15] >> 8) & 0xff, (S[:, 15] >> 16) & 0xffff
+        t_end = S[:, 13].astype(np.float64)
+        rows = len(S) // ticks
+        per = []
+        for t in range(ticks):
+            sl = slice(t * rows, (t + 1) * rows)
+            keys, inv = np.unique(simd[sl], return_inverse=True)
+            t0 = S[sl, 12].min()
+            end = np.zeros(len(keys)); nres = np.zeros(len(keys)); nt0 = np.zeros(len(keys))
+            nb = np.zeros(len(keys)); nw = np.zeros(len(keys))
+            np.maximum.at(end, inv, (t_end[sl] - t0) / 100.0)
+            np.add.at(nres, inv, res[sl]); np.add.at(nt0, inv, t0n[sl]); np.add.at(nb, inv, bul[sl])
+            np.add.at(nw, inv, 1)
+            per.append((end, nres, nt0, nb, nw))
+        end = np.concatenate([x[0] for x in per]); nres = np.concatenate([x[1] for x in per])
+        nt0 = np.concatenate([x[2] for x in per]); nb = np.concatenate([x[3] for x in per])
+        nw = np.concatenate([x[4] for x in per])
+        A = np.stack([np.ones_like(end), nres, nt0, nb / 64.0], 1)
+        coef = np.linalg.lstsq(A, end, rcond=None)[0]
+        out['simd_fit_us'] = dict(zip(['base', 'per_reset', 'per_t0', 'per_64_bullets'], coef.round(3).tolist()))
+        out['simd_end_us'] = dict(mean=float(end.mean()), p99=float(np.percentile(end, 99)), max=float(end.max()))
+        out['simd_waves'] = dict(mean=float(nw.mean()), max=float(nw.max()), min=float(nw.min()))
+        top = end >= np.percentile(end, 99)
+        out['simd_top1pct'] = dict(resets=float(nres[top].mean()), t0=float(nt0[top].mean()),
+                                   bullets=float(nb[top].mean()), waves=float(nw[top].mean()))
+        out['simd_all'] = dict(resets=float(nres.mean()), t0=float(nt0.mean()), bullets=float(nb.mean()))
     out['slow10_reset_share'] = float(((Sm[:, 9] > 0) & (Sm[:, 10] > 0)).mean())
     print(json.dumps(out), flush=True)
     _lib._lib = None
