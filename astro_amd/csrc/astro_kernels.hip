@@ -1099,6 +1099,78 @@ __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off,
         s_index[off + k - w0] = tag | (uint32_t(k) << 4) | (k == nb - 1 ? 1u << 20 : 0u);
 }
 
+// create() of one env spread over a row of 16 lanes, for PMAX <= 7: each
+// lane evaluates ONE direction() -- planet u's position angle (u < PMAX),
+// planet u - PMAX's velocity angle, or the inner ship slot's (u = 2 PMAX) --
+// and the results move by shuffles; lane s < S writes ship s, lane j < n
+// planet j (same arithmetic as create_env, bit for bit).  All lanes of the
+// row must be active; `write` gates the stores.
+template <typename T, int S, int PMAX>
+__device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroState &st, int ie,
+                                              const CreateDraws<S> &d, int u, int row0, bool write) {
+    static_assert(2 * PMAX + 1 <= 16, "one angle per lane of a 16-lane row");
+    using V = typename Store<T>::V;
+    const size_t N = size_t(st.n_env);
+    int n = d.n;
+    const bool many = n > 1;
+    const double stp = TWO_PI / double(n);
+    const double base = TWO_PI * d.u_base;
+    const double turn = double(d.reverse) * PI / 2.0;
+    const int j = u < PMAX ? u : (u < 2 * PMAX ? u - PMAX : 0);
+    const double orient = base + double(j) * stp;
+    float ang = u < PMAX ? float(orient) : float(orient + turn);
+    ang = u == 2 * PMAX ? float(TWO_PI * d.u_inner) : ang;
+    float sn, cs;
+    np_sincosf(ang, sn, cs);
+    const float is = __shfl(sn, row0 | (2 * PMAX), 64), ic = __shfl(cs, row0 | (2 * PMAX), 64);
+    const int vsrc = row0 | (PMAX + (u < PMAX ? u : 0));
+    const float vs = __shfl(sn, vsrc, 64), vc = __shfl(cs, vsrc, 64);
+
+    // ships (core.py:93-109): lane u < S writes ship u
+    const float u0 = float(d.u_out[0]) - 0.5f;
+    const float u1 = float(d.u_out[1]) - 0.5f;
+    const float o0 = p.outer_pos * (u0 > 0.0f ? 1.0f : (u0 < 0.0f ? -1.0f : 0.0f));
+    const float o1 = p.outer_pos * (u1 > 0.0f ? 1.0f : (u1 < 0.0f ? -1.0f : 0.0f));
+    const float i0 = p.inner_pos * is, i1 = p.inner_pos * ic;
+    const bool outer_first = d.u_choice < 0.5;
+    const bool second = S == 2 && u == 1;
+    float sx, sy;
+    if (n == 1) {
+        sx = second ? -o0 : o0;
+        sy = second ? -o1 : o1;
+    } else {
+        const bool outer = second ? !outer_first : outer_first;
+        sx = outer ? o0 : i0;
+        sy = outer ? o1 : i1;
+    }
+    const float b = 6.2831855f * float(second ? d.u_bear[S - 1] : d.u_bear[0]);
+    if (write && u < S) {
+        V v;
+        v.x = T(sx);
+        v.y = T(sy);
+        v.z = T(0);
+        v.w = T(0);
+        reinterpret_cast<V *>(st.ships)[size_t(u) * N + ie] = v;
+        reinterpret_cast<T *>(st.ships_b)[size_t(u) * N + ie] = T(b);
+    }
+    // planets (core.py:111-121): lane j < n writes planet j
+    if (write && u < PMAX) {
+        V v;
+        if (!many) {
+            v.x = v.y = v.z = v.w = T(0);
+        } else {
+            const double amp = sqrt(p.gravity * p.planet_mass * double(n - 1) / 2.0);
+            v.x = T(p.planet_orbit * sn);
+            v.y = T(p.planet_orbit * cs);
+            v.z = T(amp * double(vs));
+            v.w = T(amp * double(vc));
+        }
+        if (u < n) reinterpret_cast<V *>(st.planets)[size_t(u) * N + ie] = v;
+    }
+    if (n > PMAX) n = PMAX;
+    return n;
+}
+
 // One pass of the quad kernel's auto-reset: the next game (core.py:83,
 // 86-135) of up to four finished envs at once, 16 lanes per env (row r of
 // the wave serves the r-th lowest leader lane in `todo`).  create()'s draws
@@ -1135,13 +1207,14 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     // init-key chains: even lanes run key[0..] from the seed, odd lanes key[397..]
     const uint32_t k397 = hk ? key : mt_key_at(seed, 0, MT_PROLOGUE);
     const bool bchain = u & 1;
-    uint32_t x = bchain ? k397 : seed;
     const uint32_t koff = bchain ? 397u : 0u;
-    if (u < 2) s_chain[row][u][0] = x;
+    uint32_t xs[NW + 1];
+    xs[0] = bchain ? k397 : seed;
 #pragma unroll
-    for (int k = 0; k < NW; ++k) {
-        x = mt_key_next(x, koff + uint32_t(k + 1));
-        if (u < 2) s_chain[row][u][k + 1] = x;
+    for (int k = 0; k < NW; ++k) xs[k + 1] = mt_key_next(xs[k], koff + uint32_t(k + 1));
+    if (u < 2) {
+#pragma unroll
+        for (int k = 0; k <= NW; ++k) s_chain[row][u][k] = xs[k];
     }
     __syncthreads();
     const int uw = u < NW ? u : 0;
@@ -1180,9 +1253,13 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     d.reverse = many && (w_rev & 1u) == 0 ? -1 : 1;
     d.exhausted = false;   // NW outputs, far below the 227 the lazy generator covers
 
+    int n, cf = 0;
+    if constexpr (2 * PMAX + 1 <= 16) {
+        n = create_env_row<T, S, PMAX>(p, st, ie, d, u, row0, on && fast);
+    } else {
+        if (on && fast) n = create_env<T, S, PMAX, 16>(p, st, ie, d, cf, u);
+    }
     if (on && fast) {
-        int cf = 0;
-        const int n = create_env<T, S, PMAX, 16>(p, st, ie, d, cf, u);
         if (u == 0) {   // the stream record and header, as restart_env
             MTLazy g;
             g.a = c.x;

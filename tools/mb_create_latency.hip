@@ -26,6 +26,25 @@ __global__ void k_create(AstroParams p, AstroState st, int reps, unsigned long l
     if (lane == 0) cyc[i] = (t1 - t0) / reps;
 }
 
+// one env's auto-reset pass as the quad kernel runs it (1 wave per SIMD)
+__global__ void k_pass(AstroParams p, AstroState st, int reps, unsigned long long *cyc) {
+    __shared__ uint32_t s_chain[4][2][13 + 2 * 2];
+    __shared__ int s_serial[16];
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x;
+    const uint32_t seed0 = 1000u + uint32_t(i);
+    unsigned long long t0 = __builtin_readcyclecounter();
+    for (int k = 0; k < reps; ++k) {
+        const uint32_t seed = seed0 + 7919u * uint32_t(k);
+        uint64_t todo = 1;   // lane 0 = the leader of env i's quad
+        while (todo)
+            todo = wave_reset_pass<float, 2, 4>(p, st, todo, lane, i, seed, seed * 2654435761u, true, s_chain,
+                                                s_serial);
+    }
+    unsigned long long t1 = __builtin_readcyclecounter();
+    if (lane == 0) cyc[i] = (t1 - t0) / reps;
+}
+
 __global__ void k_cdraws(AstroParams p, double *out, int reps, unsigned long long *cyc) {
     if (threadIdx.x != 0) return;
     uint32_t seed = 1000u + blockIdx.x;
@@ -105,6 +124,8 @@ int main() {
     show("one MT word (dependent)");
     hipLaunchKernelGGL(k_sincos, waves, 64, 0, 0, (float *)u, 64, cyc);
     show("one np_sincosf (dependent)");
+    hipLaunchKernelGGL(k_pass, waves, 64, 0, 0, p, st, 16, cyc);
+    show("wave reset pass, 1 env");
     hipLaunchKernelGGL(k_cdraws, waves, 64, 0, 0, p, (double *)ships, 16, cyc);
     show("create's words+draws, vector");
     hipLaunchKernelGGL(k_create<1>, waves, 64, 0, 0, p, st, 16, cyc);
