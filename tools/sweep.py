@@ -202,6 +202,12 @@ def main():
             run(lib + ':c2_noreset', D._replace(reload_time=1000), 65536, auto_reset=False)
             run(lib + ':c3_262k', D, 262144)
         return
+    if a.set == 'timing':   # plain timings of alternative builds (e.g. -DASTRO_ABLATE_* ablations)
+        for lib in a.libs.split(','):
+            use_lib(lib + '.so')
+            run(lib + ':c3', D, 65536)
+            run(lib + ':c3_noreset', D, 65536, auto_reset=False)
+        return
     if a.set == 'variants':
         for lib in a.libs.split(','):
             use_lib(lib + '.so')
