@@ -1530,9 +1530,18 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                 by[2 * u + 1] = v.w;
             }
             const float xf = valid ? float(cur.x) : FAR_POS, yf = valid ? float(cur.y) : FAR_POS;
-            bool bh = false, amb = false, hs[S];
+            // float32 prefilter.  Planets only matter through the nearest one:
+            // below the band it is a certain hit, inside the band the exact
+            // tests run, above it no planet is hit.  Ships one by one (rewards)
+            float pmin = __builtin_huge_valf();
 #pragma unroll
-            for (int j = 0; j < PMAX; ++j) bh |= near32(xf, yf, bx[S + j], by[S + j], gp, amb);
+            for (int j = 0; j < PMAX; ++j) {
+                const float dx = xf - bx[S + j], dy = yf - by[S + j];
+                pmin = __builtin_fminf(pmin, dx * dx + dy * dy);
+            }
+            bool bh = pmin < gp.lo;
+            bool amb = (pmin >= gp.lo) & (pmin <= gp.hi);
+            bool hs[S];
 #pragma unroll
             for (int s = 0; s < S; ++s) hs[s] = near32(xf, yf, bx[s], by[s], gs, amb);
             amb |= valid & bt0;
@@ -1557,11 +1566,13 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                     bh = bh64;
                 }
             }
-            int hb = 0;
+            bool ship_hit = false;
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                bh |= hs[s];
-                hb |= hs[s] ? 1 << s : 0;
+            for (int s = 0; s < S; ++s) ship_hit |= hs[s];
+            bh |= ship_hit;
+            if (__any(ship_hit)) {   // rare: record which ships of the env were hit
+                const int hb = (hs[0] ? 1 : 0) | (S == 2 && hs[S - 1] ? 2 : 0);
+                if (hb) atomicOr(&s_hit[be], hb);   // (an invalid lane never hits: it sits at FAR_POS)
             }
             bool keep;
             V out;
@@ -1575,13 +1586,14 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                 out.z = T(ndx);
                 out.w = T(ndy);
             } else {
-                const double ndx = double(cur.z) + 0.0, ndy = double(cur.w) + 0.0;
-                const double nx = double(cur.x) + dt * ndx, ny = double(cur.y) + dt * ndy;
-                keep = (-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0);
+                // dx + 0 * dt in the state's own type: exact either way
+                const T ndx = cur.z + T(0), ndy = cur.w + T(0);
+                const double nx = double(cur.x) + dt * double(ndx), ny = double(cur.y) + dt * double(ndy);
+                keep = (__builtin_fabs(nx) <= 1.0) || (__builtin_fabs(ny) <= 1.0);   // -1 <= v <= 1
                 out.x = T(nx);
                 out.y = T(ny);
-                out.z = T(ndx);
-                out.w = T(ndy);
+                out.z = ndx;
+                out.w = ndy;
             }
             keep = keep & valid & !bh;
             const uint64_t kb = __ballot(keep);
@@ -1591,7 +1603,6 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
             const int pos = kg - k0;
             if (keep) bullets[size_t(base + be) * BC + pos] = out;
             if (valid && bw_last(bw)) s_kept[be] = pos + int(keep);
-            if (valid && hb) atomicOr(&s_hit[be], hb);
             carry = __builtin_amdgcn_readlane(k0, 63);
             kept_before += __popcll(kb);
           }
