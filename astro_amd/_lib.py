@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'reserved')
@@ -73,6 +73,8 @@ _SYMBOLS = {
                                          ctypes.c_void_p]),
     'astro_keytable_build': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_void_p]),
+    'astro_features': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
+                                      ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -1802,6 +1802,68 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     }
 }
 
+// ---------------------------------------------------------------------------
+// Observation features: rl.ValueNetwork.get_features + to_batch
+// (rl.py:36-112), one lane per (env, row).  The bearing feature is
+// util.norm_angle(b) / pi (util.py:125-132) in the precision numpy uses: float32
+// for create()'s float32 ships (tick 0), float64 after; every value is then
+// stored as float32, as the reference's float32 feature array does.
+
+// ((b + pi) % (2 pi) - pi) / pi with numpy's floored remainder
+// (npy_divmod: fmod, + divisor when the signs differ, +0 for a zero result)
+template <typename C>
+__device__ __forceinline__ C norm_angle_over_pi(C b) {
+    const C pi = C(3.141592653589793);          // np.pi (float32: 3.1415927f)
+    const C two_pi = C(6.283185307179586);      // 2 * np.pi
+    const C x = b + pi;
+    C m = fmod(x, two_pi);
+    m = m != C(0) ? (m < C(0) ? m + two_pi : m) : C(0);
+    return (m - pi) / pi;
+}
+
+template <typename T, int S>
+__global__ __launch_bounds__(256) void astro_features_kernel(AstroParams p, AstroState st, float *__restrict__ out,
+                                                             int rows) {
+    using V = typename Store<T>::V;
+    constexpr int D = 1 + 5 * S + 4;
+    const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    const int N = st.n_env;
+    if (idx >= int64_t(N) * rows) return;
+    const int i = int(idx / rows), r = int(idx - int64_t(i) * rows);
+    const size_t NN = size_t(N);
+    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+    int np = h.y & 0xff;
+    np = np < 1 ? 1 : (np > p.p_pad ? p.p_pad : np);
+    const int nb = min(int(uint32_t(h.y) >> 16), p.b_cap);
+    const bool t0 = (uint32_t(h.x) & TICK_MASK) == 0;
+    float f[D];
+    if (r >= np + nb) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) f[k] = -1.0f;   // to_batch padding
+    } else {
+        f[0] = r < np ? 0.0f : 1.0f;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const V v = reinterpret_cast<const V *>(st.ships)[size_t(s) * NN + i];
+            const T b = reinterpret_cast<const T *>(st.ships_b)[size_t(s) * NN + i];
+            f[1 + 5 * s] = float(v.x);
+            f[2 + 5 * s] = float(v.y);
+            f[3 + 5 * s] = float(v.z);
+            f[4 + 5 * s] = float(v.w);
+            f[5 + 5 * s] = t0 ? norm_angle_over_pi<float>(float(b)) : float(norm_angle_over_pi<double>(double(b)));
+        }
+        const V o = r < np ? reinterpret_cast<const V *>(st.planets)[size_t(r) * NN + i]
+                           : reinterpret_cast<const V *>(st.bullets)[size_t(i) * size_t(p.b_cap) + (r - np)];
+        f[1 + 5 * S] = float(o.x);
+        f[2 + 5 * S] = float(o.y);
+        f[3 + 5 * S] = float(o.z);
+        f[4 + 5 * S] = float(o.w);
+    }
+    float *dst = out + idx * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) dst[k] = f[k];
+}
+
 template <typename T, int S, int PMAX>
 __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, AstroState st,
                                                             const uint32_t *__restrict__ seeds,
@@ -1959,6 +2021,15 @@ int dispatch(const AstroParams &p, const AstroState &s, A... a) {
 }
 
 template <typename T, int S, int PM>
+struct FeatL {   // (no PMAX dependence: one instance per T, S)
+    static int run(const AstroParams &p, const AstroState &s, float *out, int rows, hipStream_t st) {
+        const int64_t lanes = int64_t(s.n_env) * rows;
+        hipLaunchKernelGGL((astro_features_kernel<T, S>), dim3(unsigned((lanes + 255) / 256)), dim3(256), 0, st, p, s,
+                           out, rows);
+        return launched("astro_features");
+    }
+};
+template <typename T, int S, int PM>
 struct StepL {
     static int run(const AstroParams &p, const AstroState &s, const int8_t *c, float *r, uint8_t *d,
                    uint64_t *stats, int ar, hipStream_t st) {
@@ -2029,6 +2100,17 @@ int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *s
     hipLaunchKernelGGL(astro_stream_init_kernel, dim3(grid), dim3(BLOCK), 0,
                        reinterpret_cast<hipStream_t>(stream), *s, stream_seeds);
     return launched("astro_stream_init");
+}
+
+int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_t rows, void *stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if ((rc = check_state(s))) return rc;
+    if (s->n_env == 0) return 0;
+    if (!out || (reinterpret_cast<uintptr_t>(out) & 3u)) return fail(-60, "out is NULL or not 4-byte aligned");
+    if (rows < 1) return fail(-61, "rows must be >= 1");
+    if (int64_t(s->n_env) * rows > (int64_t(1) << 40)) return fail(-62, "n_env * rows too large");
+    return dispatch<FeatL>(*p, *s, out, int(rows), reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -209,6 +209,25 @@ class BatchedEnv:
             planets=self.planets.permute(1, 0, 2), nplanets=self.nplanets,
             bullets=self.bullets, nbullets=self.nbullets, tick=self.tick)
 
+    def features(self, rows=None, out=None):
+        """Observation features of every env, as rl.ValueNetwork.get_features
+        then to_batch (rl.py:36-112): float32 [N, rows, 1 + 5*S + 4], rows
+        [planets, live bullets] then -1 padding; column 0 is the object type
+        (0 planet, 1 bullet, -1 padding), then every ship's (x, y, dx, dy,
+        norm_angle(b)/pi), then the object's (x, y, dx, dy).  rows defaults
+        to p_pad + b_cap, which holds every env's objects."""
+        rows = self.p_pad + self.b_cap if rows is None else int(rows)
+        D = 1 + 5 * self.S + 4
+        if out is None:
+            out = torch.empty((self.n_env, rows, D), dtype=torch.float32, device=self.device)
+        elif (tuple(out.shape) != (self.n_env, rows, D) or out.dtype != torch.float32
+              or out.device != self.device or not out.is_contiguous()):
+            raise ValueError('out must be a contiguous float32 [%d, %d, %d] tensor on %s'
+                             % (self.n_env, rows, D, self.device))
+        _lib.check(self.lib.astro_features(ctypes.byref(self.params), ctypes.byref(self.state),
+                                           out.data_ptr(), rows, _stream_ptr(self.device)), 'astro_features')
+        return out
+
     def stat_dict(self):
         v = self.stats.sum(0).cpu().tolist()
         return dict(zip(_lib.STAT_NAMES, v))

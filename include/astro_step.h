@@ -11,6 +11,8 @@
  *                         env's generate_configs stream), core.py:77-135)
  *   astro_reset        <- core.create(config)                 core.py:86-135
  *   astro_stream_init  <- core.generate_configs(config)       core.py:77-83
+ *   astro_features     <- rl.ValueNetwork.get_features(state) + to_batch
+ *                         (rl.py:36-112), the observation a policy consumes
  *
  * Conventions
  *   - The caller owns and allocates all device memory (e.g. PyTorch
@@ -20,9 +22,10 @@
  *   - Return 0 on success, a negative code on a bad argument (-1..-99) or a
  *     launch failure (-1000 - hipError_t).  astro_last_error() describes the
  *     last failure of the calling thread.
- *   - State is struct-of-arrays, entity-major: slot s of env i lives at
- *     [s * n_env + i], so consecutive lanes (envs) touch consecutive bytes.
- *     Element type is float (state_f64 = 0) or double (state_f64 = 1).
+ *   - Ships and planets are struct-of-arrays, entity-major: slot s of env i
+ *     lives at [s * n_env + i], so consecutive lanes (envs) touch consecutive
+ *     bytes; bullets are one contiguous row per env.  Element type is float
+ *     (state_f64 = 0) or double (state_f64 = 1).
  */
 #ifndef ASTRO_STEP_H
 #define ASTRO_STEP_H
@@ -33,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 5
+#define ASTRO_ABI_VERSION 6
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -137,6 +140,15 @@ int astro_keytable_build(uint32_t *table, uint32_t first, uint32_t count, void *
 /* Position env i's seed stream at generate_configs(seed=stream_seeds[i]) and
  * queue its first game (the next astro_reset without seeds creates it). */
 int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *stream);
+
+/* Observation features of every env, as rl.ValueNetwork.get_features then
+ * to_batch (rl.py:36-112): out float [n_env][rows][1 + 5*nships + 4]; row r <
+ * nplanets is planet r, then the live bullets; column 0 = 0 planet / 1
+ * bullet, then every ship's (x, y, dx, dy, norm_angle(b)/pi), then the
+ * object's (x, y, dx, dy); rows past the env's objects are -1 (to_batch's
+ * padding).  rows = p_pad + b_cap always suffices; objects past `rows` are
+ * left out. */
+int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_t rows, void *stream);
 
 #ifdef __cplusplus
 }

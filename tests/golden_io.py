@@ -97,3 +97,23 @@ def games():
             g[f] = z[key + '__' + f]
         out.append(g)
     return out
+
+
+class Features:
+    """rl.ValueNetwork.get_features of every input state of steps.npz, and a
+    few to_batch results (tools/gen_golden.py: gen_features)."""
+
+    def __init__(self):
+        z = load('features.npz')
+        self.z = {k: z[k] for k in z.files}
+
+    def of(self, i):
+        z = self.z
+        a, b = z['features_off'][i], z['features_off'][i + 1]
+        return z['features'][a:b, :z['dims'][i]]
+
+    def batches(self):
+        k = 0
+        while 'batch_%d' % k in self.z:
+            yield self.z['batch_idx_%d' % k], self.z['batch_%d' % k]
+            k += 1

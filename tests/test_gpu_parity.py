@@ -358,3 +358,51 @@ def test_without_key_table_identical(kernel):
         assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), f
     assert torch.equal(envs[0].hdr[:, 1], envs[1].hdr[:, 1])
     assert envs[0].stat_dict()['resets'] > 0
+
+
+# ------------------------------------------------- observation features
+
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+def test_features_match_reference(dtype):
+    """astro_features on every golden input state == rl.ValueNetwork
+    .get_features of the reference, bit for bit (float32 state: the golden
+    inputs are float32-valued, so the stored values are identical), with
+    to_batch's -1 padding after each env's objects."""
+    tr = gio.Transitions('steps.npz')
+    fx = gio.Features()
+    for name, idx in tr.groups():
+        cfg = CFG[name]
+        S = 1 if cfg.solo else 2
+        bcap = tr.max_bullets(idx) + 2
+        B = tr.batch_in(idx, S, b_cap=bcap)
+        env = _env(cfg, idx.size, dtype=dtype, b_cap=bcap)
+        env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
+        got = env.features().cpu().numpy()
+        assert got.shape == (idx.size, env.p_pad + bcap, 1 + 5 * S + 4)
+        for r, i in enumerate(idx):
+            want = fx.of(i)
+            assert np.array_equal(got[r, :want.shape[0]].view(np.uint32), want.view(np.uint32)), (name, i)
+            assert (got[r, want.shape[0]:] == -1).all(), (name, i)
+
+
+def test_features_batched_run_vs_oracle():
+    """Features of a float32 auto-reset run (fresh games at tick 0 every
+    step) == the oracle's, each tick; a cut `rows` keeps the first objects."""
+    from oracle import features
+    cfg = CFG['rapid']
+    n = 999
+    env = _env(cfg, n, dtype=torch.float32, b_cap=24, p_pad=4, auto_reset=True)
+    env.reset()
+    rng = np.random.RandomState(5)
+    for t in range(25):
+        B = _host_batch(env)
+        rows = env.p_pad + env.b_cap
+        assert np.array_equal(env.features().cpu().numpy(), features.batched(B, env.S, rows)), t
+        if t % 8 == 3:
+            assert np.array_equal(env.features(rows=5).cpu().numpy(), features.batched(B, env.S, 5)), t
+        ctl = rng.randint(0, 6, size=(n, env.S)).astype(np.int8)
+        env.step(torch.from_numpy(ctl).cuda())
+    out = torch.empty((n, 28, 15), dtype=torch.float32, device='cuda:0')
+    assert env.features(out=out) is out
+    with pytest.raises(ValueError):
+        env.features(out=torch.empty((n, 27, 15), dtype=torch.float32, device='cuda:0'))

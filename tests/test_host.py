@@ -32,7 +32,7 @@ def _declared_functions():
 def test_library_exports_every_header_symbol(lib):
     names = _declared_functions()
     assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_reset',
-                          'astro_stream_init', 'astro_keytable_build'}
+                          'astro_stream_init', 'astro_keytable_build', 'astro_features'}
     out = subprocess.check_output(['nm', '-D', '--defined-only', _lib.LIB_PATH], text=True)
     exported = set(re.findall(r' T (astro_\w+)$', out, re.M))
     assert set(names) <= exported
@@ -79,6 +79,9 @@ def test_argument_validation_without_gpu(lib):
     assert lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None) == 0
     assert lib.astro_stream_init(ctypes.byref(s), None, None) == 0
     assert lib.astro_step(None, ctypes.byref(s), None, None, None, None, 0, None) == -10
+    assert lib.astro_features(ctypes.byref(p), ctypes.byref(s), None, 0, None) == 0   # empty batch
+    s.n_env = 4
+    assert lib.astro_features(ctypes.byref(p), ctypes.byref(s), None, 36, None) == -4  # arrays NULL
     assert lib.astro_keytable_build(None, 0, 16, None) == -50
     assert lib.astro_keytable_build(ctypes.c_void_p(16), (1 << 30) - 8, 16, None) == -51
 

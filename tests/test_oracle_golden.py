@@ -218,3 +218,50 @@ def test_port_create_bit_exact():
             n = s.planets.x.shape[0]
             assert np.array_equal(s.ships.x, z[name + '__ships_x'][k, :g.ns])
             assert np.array_equal(s.planets.dx, z[name + '__planets_dx'][k, :n])
+
+
+# ------------------------------------------------- observation features
+
+def test_features_golden_bit_exact():
+    """oracle.features.get_features == rl.ValueNetwork.get_features
+    (rl.py:43-72) on all 8,812 golden input states, bit for bit (float32
+    bearings at tick 0, float64 after)."""
+    from oracle import features
+    tr = gio.Transitions('steps.npz')
+    fx = gio.Features()
+    for i in range(tr.n):
+        S = int(tr.z['nships'][i])
+        got = features.get_features(_state_from_row(tr, i, S))
+        want = fx.of(i)
+        assert got.shape == want.shape and got.dtype == np.float32
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), i
+
+
+def test_features_to_batch_golden():
+    """to_batch (rl.py:75-99): -1 padding to the longest member."""
+    from oracle import features
+    tr = gio.Transitions('steps.npz')
+    fx = gio.Features()
+    for idx, want in fx.batches():
+        got = features.to_batch([fx.of(int(i)) for i in idx])
+        assert np.array_equal(got, want)
+    with pytest.raises(ValueError):
+        features.to_batch([np.zeros((2, 15), np.float32), np.zeros((2, 10), np.float32)])
+
+
+def test_features_batched_equals_per_state():
+    """The batched form (what the kernel is checked against) agrees with the
+    per-state restatement on a golden group, padding included."""
+    from oracle import features
+    tr = gio.Transitions('steps.npz')
+    fx = gio.Features()
+    for name, idx in tr.groups():
+        S = 1 if CFG[name].solo else 2
+        idx = idx[:200]
+        B = tr.batch_in(idx, S)
+        rows = 8 + B.bullets.shape[1]
+        got = features.batched(B, S, rows)
+        for r, i in enumerate(idx):
+            want = fx.of(i)
+            assert np.array_equal(got[r, :want.shape[0]], want), (name, i)
+            assert (got[r, want.shape[0]:] == -1).all()

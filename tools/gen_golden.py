@@ -7,7 +7,8 @@ Test infrastructure only.  This script imports DouglasOrr/Astro's own
 ``astro/__init__.py``'s imports of ``rl``/``server`` -- which need the absent
 ``tensorboardX``/``lru`` -- are skipped) and records inputs and outputs of
 ``core.create`` (core.py:86-135), ``core.generate_configs`` (core.py:77-83) and
-``core.step`` (core.py:215-303) as small ``.npz``/``.json`` fixtures.
+``core.step`` (core.py:215-303), and ``rl.ValueNetwork.get_features`` /
+``to_batch`` (rl.py:36-112), as small ``.npz``/``.json`` fixtures.
 
 It refuses to run when ``/root/reference`` is absent, so it never runs on the
 GPU box; the fixtures it writes are plain data (inputs + expected outputs) and
@@ -461,7 +462,131 @@ def gen_kats():
     print('wrote kat.json')
 
 
+# ---------------------------------------------------------------------------
+# 6. Observation features: rl.ValueNetwork.get_features / to_batch
+#    (rl.py:36-112) of every input state of steps.npz
+
+def _import_rl():
+    """astro/rl.py imports tensorboardX at module level for its training
+    logger; it is absent here and unused by get_features/to_batch, so an empty
+    placeholder module is registered before the import (nothing of rl.py's
+    feature code is touched)."""
+    sys.modules.setdefault('tensorboardX', types.ModuleType('tensorboardX'))
+    from astro import rl  # noqa: E402
+    return rl
+
+
+def gen_features():
+    rl = _import_rl()
+    z = np.load(os.path.join(OUT, 'steps.npz'))
+    names = list(z['cfg_names'])
+    feats, rows, dims = [], [], []
+    for i in range(z['tick'].shape[0]):
+        S = int(z['nships'][i])
+        npl = int(z['nplanets'][i])
+        fl = int(z['dtype_flags'][i])
+        sh = z['in_ships'][i, :S]
+        pl = z['in_planets'][i, :npl]
+        off = z['in_bullets_off']
+        bl = z['in_bullets'][off[i]:off[i + 1]]
+        f32 = np.float32
+        sdt = f32 if fl & 1 else np.float64
+        B = core.Bodies
+        state = core.State(
+            ships=B(x=sh[:, 0:2].astype(sdt), dx=sh[:, 2:4].astype(sdt), b=sh[:, 4].astype(sdt)),
+            planets=B(x=pl[:, 0:2].astype(f32 if fl & 2 else np.float64),
+                      dx=pl[:, 2:4].astype(f32 if fl & 4 else np.float64), b=None),
+            bullets=B(x=bl[:, 0:2].astype(f32 if fl & 8 else np.float64),
+                      dx=bl[:, 2:4].astype(f32 if fl & 8 else np.float64), b=None),
+            reload=0.0, t=0.0)
+        f = rl.ValueNetwork.get_features(state)
+        assert f.dtype == np.float32
+        feats.append(f)
+        rows.append(f.shape[0])
+        dims.append(f.shape[1])
+    off = np.zeros(len(rows) + 1, dtype=np.int64)
+    off[1:] = np.cumsum(rows)
+    flat = np.zeros((int(off[-1]), 15), dtype=np.float32)
+    for i, f in enumerate(feats):
+        flat[off[i]:off[i + 1], :f.shape[1]] = f
+    # to_batch of a few groups of same-ship-count states (ragged rows -> -1 padding)
+    groups, batches = [], []
+    for name in ('default', 'solo', 'rapid'):
+        idx = [i for i in range(len(rows)) if names[z['cfg'][i]] == name][:40:5]
+        b = rl.ValueNetwork.to_batch([feats[i] for i in idx])
+        groups.append(np.array(idx, dtype=np.int64))
+        batches.append(b)
+    np.savez_compressed(os.path.join(OUT, 'features.npz'), features=flat, features_off=off,
+                        dims=np.array(dims, dtype=np.int32),
+                        **{'batch_idx_%d' % k: g for k, g in enumerate(groups)},
+                        **{'batch_%d' % k: b for k, b in enumerate(batches)})
+    print('wrote features.npz', len(rows), 'states', int(off[-1]), 'rows')
+
+
+# ---------------------------------------------------------------------------
+# 7. A game log written by the reference (core.save_log, core.py:413-426)
+
+def gen_log():
+    config = CONFIGS['short']
+    game = core.play(config, [script.NothingBot(), script.NothingBot()])
+    import gzip
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, 'log.jsonl')
+        core.save_log(path, game)
+        data = open(path, 'rb').read()
+    with gzip.GzipFile(os.path.join(OUT, 'log_short_nothing.jsonl.gz'), 'wb', mtime=0) as f:
+        f.write(data)
+    print('wrote log_short_nothing.jsonl.gz', len(game.ticks), 'ticks, winner', game.winner)
+
+
+# ---------------------------------------------------------------------------
+# 8. ScriptBot decisions (script.py:13-83) on every input state of steps.npz,
+#    for each ship's ego view (core.roll_ships, core.py:306-327)
+
+def gen_script_controls():
+    z = np.load(os.path.join(OUT, 'steps.npz'))
+    names = list(z['cfg_names'])
+    out = np.full((z['tick'].shape[0], S_PAD), -1, dtype=np.int8)
+    bots = {}
+    for i in range(z['tick'].shape[0]):
+        name = names[z['cfg'][i]]
+        config = CONFIGS[name]
+        if name not in bots:
+            bots[name] = script.ScriptBot.create(config)
+        S = int(z['nships'][i])
+        npl = int(z['nplanets'][i])
+        fl = int(z['dtype_flags'][i])
+        sh = z['in_ships'][i, :S]
+        pl = z['in_planets'][i, :npl]
+        off = z['in_bullets_off']
+        bl = z['in_bullets'][off[i]:off[i + 1]]
+        f32 = np.float32
+        sdt = f32 if fl & 1 else np.float64
+        B = core.Bodies
+        state = core.State(
+            ships=B(x=sh[:, 0:2].astype(sdt), dx=sh[:, 2:4].astype(sdt), b=sh[:, 4].astype(sdt)),
+            planets=B(x=pl[:, 0:2].astype(f32 if fl & 2 else np.float64),
+                      dx=pl[:, 2:4].astype(f32 if fl & 4 else np.float64), b=None),
+            bullets=B(x=bl[:, 0:2].astype(f32 if fl & 8 else np.float64),
+                      dx=bl[:, 2:4].astype(f32 if fl & 8 else np.float64), b=None),
+            reload=0.0, t=0.0)
+        for k in range(S):
+            out[i, k] = bots[name](core.roll_ships(state, k))
+    np.savez_compressed(os.path.join(OUT, 'script_controls.npz'), control=out)
+    print('wrote script_controls.npz', out.shape[0], 'states')
+
+
 def main():
+    if sys.argv[1:] == ['script']:
+        gen_script_controls()
+        return
+    if sys.argv[1:] == ['features']:
+        gen_features()
+        return
+    if sys.argv[1:] == ['log']:
+        gen_log()
+        return
     os.makedirs(OUT, exist_ok=True)
     np.random.seed(0)
     with open(os.path.join(OUT, 'configs.json'), 'w') as f:
@@ -472,6 +597,9 @@ def main():
     gen_edges()
     gen_steps()
     gen_games()
+    gen_features()
+    gen_log()
+    gen_script_controls()
 
 
 if __name__ == '__main__':
