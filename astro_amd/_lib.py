@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'reserved')
@@ -61,6 +61,18 @@ class AstroState(ctypes.Structure):
     ]
 
 
+class AstroPolicy(ctypes.Structure):
+    _fields_ = [
+        ('kind', ctypes.c_int32),
+        ('reserved', ctypes.c_int32),
+        ('seed', ctypes.c_uint64),
+        ('tick0', ctypes.c_int64),
+        ('env_offset', ctypes.c_int64),
+    ]
+
+
+POLICIES = {'control': 0, 'nothing': 1, 'random': 2}
+
 _SYMBOLS = {
     'astro_abi_version': (ctypes.c_int, []),
     'astro_last_error': (ctypes.c_char_p, []),
@@ -75,6 +87,10 @@ _SYMBOLS = {
                                             ctypes.c_void_p]),
     'astro_features': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    'astro_rollout': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
+                                     ctypes.POINTER(AstroPolicy), ctypes.c_int32, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                     ctypes.c_void_p]),
 }
 
 _lib = None

@@ -620,6 +620,34 @@ constexpr int NSTAMP = 16;
 #endif
 
 constexpr int BLOCK = 64;
+
+// Where a launch's controls come from and how many ticks it runs
+// (astro_step: one tick of a control array; astro_rollout: K ticks of a
+// control array or of an on-device policy).
+struct TickDriver {
+    const int8_t *control;   // ASTRO_POLICY_CONTROL: int8 [ticks][n_env][nships]
+    int32_t policy;          // ASTRO_POLICY_*
+    int32_t ticks;           // >= 1 (the lane kernel runs 1 per launch)
+    uint64_t seed;           // ASTRO_POLICY_RANDOM
+    int64_t tick0;           // ASTRO_POLICY_RANDOM: number of the launch's first tick
+    int64_t env_offset;      // ASTRO_POLICY_RANDOM: global id of env 0
+};
+
+// Control of ship s of env i at tick kt of the launch.  RANDOM is uniform in
+// [0, 6) from splitmix64(global ship id, tick) -- bench.py's `controls`.
+template <int S>
+__device__ __forceinline__ int tick_control(const TickDriver &d, int i, int s, size_t n_env, int kt) {
+    if (d.policy == ASTRO_POLICY_CONTROL) return int(d.control[(size_t(kt) * n_env + size_t(i)) * S + s]);
+    if (d.policy == ASTRO_POLICY_RANDOM) {
+        const uint64_t id = uint64_t(d.env_offset + i) * uint64_t(S) + uint64_t(s);
+        uint64_t z = id * 0x9E3779B97F4A7C15ull + uint64_t(d.tick0 + kt + 1) * 0xD1B54A32D192ED03ull + d.seed;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        return int(((z >> 32) * 6ull) >> 32);
+    }
+    return 2;   // ASTRO_POLICY_NOTHING: script.NothingBot
+}
 constexpr int BCHUNK = 8;  // bullets loaded per batch: 8 loads in flight per lane
 
 // One bullet pass in precision C (float at tick 0, double after): collide
@@ -740,8 +768,7 @@ __device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V
 }
 
 template <typename T, int S, int PMAX>
-__global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroState st,
-                                                           const int8_t *__restrict__ control,
+__global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                            float *__restrict__ reward,
                                                            uint8_t *__restrict__ done_out,
                                                            unsigned long long *stats,
@@ -782,13 +809,14 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             sdy[s] = double(v.w);
             sb[s] = double(ships_b[size_t(s) * NN + i]);
         }
-        int ctl[S];
-        if (S == 2) {
-            const uint16_t c2 = reinterpret_cast<const uint16_t *>(control)[i];
+        int ctl[S];   // (one tick per launch: the host loops astro_rollout's ticks)
+        if (S == 2 && drv.policy == ASTRO_POLICY_CONTROL) {
+            const uint16_t c2 = reinterpret_cast<const uint16_t *>(drv.control)[i];
             ctl[0] = int(int8_t(c2 & 0xff));
             ctl[S - 1] = int(int8_t(c2 >> 8));
         } else {
-            ctl[0] = int(control[i]);
+#pragma unroll
+            for (int s = 0; s < S; ++s) ctl[s] = tick_control<S>(drv, i, s, NN, 0);
         }
         const int tick = int(uint32_t(h.x) & TICK_MASK);
         const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
@@ -1295,11 +1323,10 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     return todo;
 }
 
-template <typename T, int S, int PMAX>
-__global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st,
-                                                                const int8_t *__restrict__ control,
-                                                                float *__restrict__ reward,
-                                                                uint8_t *__restrict__ done_out,
+template <typename T, int S, int PMAX, bool MULTI>
+__global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+                                                                float *__restrict__ reward_all,
+                                                                uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {
     using V = typename Store<T>::V;
     constexpr int PPL = PMAX / 4;   // planet slots per lane
@@ -1322,22 +1349,29 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     T *ships_b = reinterpret_cast<T *>(st.ships_b);
     V *planets = reinterpret_cast<V *>(st.planets);
     V *bullets = reinterpret_cast<V *>(st.bullets);
-    uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
-    bool f_reset = false, f_coll = false, f_tout = false;
-    bool need_reset = false;   // leader lane (q == 0) of an env whose game ended, auto-reset on
+    uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;   // per lane, summed over the launch's ticks
+    uint32_t c_reset = 0, c_coll = 0, c_tout = 0;           // per wave
 #ifdef ASTRO_STAMPS
     unsigned long long stamp_[NSTAMP] = {};
 #endif
+    const int sq = q < S ? q : 0;
+    // ---- the launch's ticks: each wave steps its 16 envs on its own, no
+    //      grid-wide barrier between ticks (envs never interact)
+    const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
+    for (int kt = 0; kt < n_ticks; ++kt) {
+    float *__restrict__ reward = reward_all + size_t(kt) * NN * S;
+    uint8_t *__restrict__ done_out = done_all + size_t(kt) * NN;
+    bool f_reset = false, f_coll = false, f_tout = false;
+    bool need_reset = false;   // leader lane (q == 0) of an env whose game ended, auto-reset on
     STAMP(0);
 
     // ---- loads, all independent of each other: header, own ship (lanes <
     //      S), control, own planet slots (read whether live or not; padding
     //      is masked below)
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
-    const int sq = q < S ? q : 0;
     const V sv = ships[size_t(sq) * NN + i];
     const T sbv = ships_b[size_t(sq) * NN + i];
-    const int ctl = int(control[size_t(i) * S + sq]);
+    const int ctl = tick_control<S>(drv, i, sq, NN, kt);
     V pv[PPL];
     T mpx[PPL], mpy[PPL];
 #pragma unroll
@@ -1360,7 +1394,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
     uint32_t pend_key = uint32_t(h.w);
     if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
-    n_pl = active && q == 0 ? uint32_t(np) : 0u;
+    n_pl += active && q == 0 ? uint32_t(np) : 0u;
 
     // ---- index the wave's live bullets densely: bullet k of env e is number
     //      g = off_e + k, so the bullet pass below runs ceil(sum nb / 64)
@@ -1611,7 +1645,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     __syncthreads();
     const int wr_in = s_kept[e];
     const int hit_bits = s_hit[e];
-    n_bin = active && q == 0 ? uint32_t(nb) : 0u;
+    n_bin += active && q == 0 ? uint32_t(nb) : 0u;
     STAMP(4);
 
     if (active) {
@@ -1732,8 +1766,8 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
                 const uint32_t kv = (key_valid || p.key_table) ? KEY_VALID : 0u;
                 reinterpret_cast<int4 *>(st.hdr)[i] =
                     make_int4(int(uint32_t(tick + 1) | kv), np | (fl << 8) | (w << 16), int(pend_seed), int(pend_key));
-                n_bout = uint32_t(w);
-                n_drop = uint32_t(dropped);
+                n_bout += uint32_t(w);
+                n_drop += uint32_t(dropped);
             }
             STAMP(8);
         } else {
@@ -1761,7 +1795,11 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
         }
     }
     STAMP(10);
-    STAMP(11);
+    if (stats) {
+        c_reset += __popcll(__ballot(f_reset));
+        c_coll += __popcll(__ballot(f_coll));
+        c_tout += __popcll(__ballot(f_tout));
+    }
 #ifdef ASTRO_STAMPS
     {   // where the wave ran and what it carried: per-SIMD load attribution
         unsigned hw, xcc;
@@ -1772,6 +1810,11 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
         stamp_[14] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
         stamp_[15] = n_res | (n_t0 << 8) | ((unsigned long long)total << 16);
     }
+#endif
+    if (kt + 1 < n_ticks) __syncthreads();   // this tick's stores are seen by the wave's next
+    }   // ticks
+    STAMP(11);
+#ifdef ASTRO_STAMPS
     if (stats && lane == 0) {
         unsigned long long *row = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * NSTAMP;
         for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
@@ -1780,22 +1823,23 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
 #endif
 
     if (stats) {   // one private row per wave (16 envs)
-        const uint64_t m_reset = __ballot(f_reset), m_coll = __ballot(f_coll), m_tout = __ballot(f_tout);
-        const bool packed = p.b_cap <= 1023;
+        // per-lane counts and their wave sums fit 16 bits when b_cap * ticks * 16 < 2^16
+        const bool packed = uint64_t(p.b_cap) * uint64_t(n_ticks) * 16u < 65536u;
         const uint32_t a = wave_sum32(packed ? (n_bin | (n_bout << 16)) : n_bin);
         const uint32_t b = wave_sum32(packed ? (n_pl | (n_drop << 16)) : n_bout);
-        const uint32_t c = packed ? 0u : wave_sum32(n_pl | (n_drop << 16));
+        const uint32_t c = packed ? 0u : wave_sum32(n_pl);
+        const uint32_t d = packed ? 0u : wave_sum32(n_drop);
         if (lane == 0) {
             unsigned long long *slot = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * ASTRO_NSTATS;
             const uint64_t bin = packed ? (a & 0xffff) : a;
             const uint64_t bout = packed ? (a >> 16) : b;
-            const uint64_t pl = packed ? (b & 0xffff) : (c & 0xffff);
-            const uint64_t drop = packed ? (b >> 16) : (c >> 16);
+            const uint64_t pl = packed ? (b & 0xffff) : c;
+            const uint64_t drop = packed ? (b >> 16) : d;
             if (bin) atomicAdd(slot + ASTRO_STAT_BULLETS_IN, (unsigned long long)bin);
             if (bout) atomicAdd(slot + ASTRO_STAT_BULLETS_OUT, (unsigned long long)bout);
-            if (m_reset) atomicAdd(slot + ASTRO_STAT_RESETS, (unsigned long long)__popcll(m_reset));
-            if (m_coll) atomicAdd(slot + ASTRO_STAT_COLLISIONS, (unsigned long long)__popcll(m_coll));
-            if (m_tout) atomicAdd(slot + ASTRO_STAT_TIMEOUTS, (unsigned long long)__popcll(m_tout));
+            if (c_reset) atomicAdd(slot + ASTRO_STAT_RESETS, (unsigned long long)c_reset);
+            if (c_coll) atomicAdd(slot + ASTRO_STAT_COLLISIONS, (unsigned long long)c_coll);
+            if (c_tout) atomicAdd(slot + ASTRO_STAT_TIMEOUTS, (unsigned long long)c_tout);
             if (drop) atomicAdd(slot + ASTRO_STAT_OVERFLOWS, (unsigned long long)drop);
             if (pl) atomicAdd(slot + ASTRO_STAT_PLANETS, (unsigned long long)pl);
         }
@@ -1978,13 +2022,17 @@ int pick_kernel(const AstroParams &p, int n_env) {
 }
 
 template <typename T, int S, int PM>
-int launch_step(const AstroParams &p, const AstroState &s, const int8_t *c, float *r, uint8_t *d,
+int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv, float *r, uint8_t *d,
                 uint64_t *stats, int ar, hipStream_t stream) {
     unsigned long long *st = reinterpret_cast<unsigned long long *>(stats);
-    if (pick_kernel(p, s.n_env) == ASTRO_KERNEL_QUAD) {
+    if (pick_kernel(p, s.n_env) == ASTRO_KERNEL_QUAD) {   // all ticks in one launch
         const int grid = int((int64_t(s.n_env) * 4 + BLOCK - 1) / BLOCK);
-        hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, c, r, d,
-                           st, ar);
+        if (drv.ticks == 1)
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false>), dim3(grid), dim3(BLOCK), 0, stream, p, s,
+                               drv, r, d, st, ar);
+        else
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true>), dim3(grid), dim3(BLOCK), 0, stream, p, s,
+                               drv, r, d, st, ar);
         return launched("astro_step(quad)");
     }
 #ifdef ASTRO_ENVS_PER_WAVE
@@ -1993,8 +2041,17 @@ int launch_step(const AstroParams &p, const AstroState &s, const int8_t *c, floa
 #else
     const int grid = (s.n_env + BLOCK - 1) / BLOCK;
 #endif
-    hipLaunchKernelGGL((astro_step_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, c, r, d, st, ar);
-    return launched("astro_step");
+    const size_t N = size_t(s.n_env);
+    for (int k = 0; k < drv.ticks; ++k) {   // the lane kernel: one launch per tick
+        TickDriver one = drv;
+        one.ticks = 1;
+        one.tick0 = drv.tick0 + k;
+        if (drv.control) one.control = drv.control + size_t(k) * N * size_t(S);
+        hipLaunchKernelGGL((astro_step_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, one,
+                           r + size_t(k) * N * size_t(S), d + size_t(k) * N, st, ar);
+        if (int rc = launched("astro_step")) return rc;
+    }
+    return 0;
 }
 
 template <typename T, int S, int PM>
@@ -2031,9 +2088,9 @@ struct FeatL {   // (no PMAX dependence: one instance per T, S)
 };
 template <typename T, int S, int PM>
 struct StepL {
-    static int run(const AstroParams &p, const AstroState &s, const int8_t *c, float *r, uint8_t *d,
+    static int run(const AstroParams &p, const AstroState &s, const TickDriver &drv, float *r, uint8_t *d,
                    uint64_t *stats, int ar, hipStream_t st) {
-        return launch_step<T, S, PM>(p, s, c, r, d, stats, ar, st);
+        return launch_step<T, S, PM>(p, s, drv, r, d, stats, ar, st);
     }
 };
 template <typename T, int S, int PM>
@@ -2064,8 +2121,30 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
         return fail(-32, "control must be 2-byte and reward 8-byte aligned");
     if (int64_t(s->n_env) * 4 > int64_t(0x7fffffff)) return fail(-34, "n_env too large");
     if (stats && (reinterpret_cast<uintptr_t>(stats) & 7u)) return fail(-33, "stats must be 8-byte aligned");
-    return dispatch<StepL>(*p, *s, control, reward, done, stats, int(auto_reset),
-                           reinterpret_cast<hipStream_t>(stream));
+    const TickDriver drv{control, ASTRO_POLICY_CONTROL, 1, 0, 0, 0};
+    return dispatch<StepL>(*p, *s, drv, reward, done, stats, int(auto_reset), reinterpret_cast<hipStream_t>(stream));
+}
+
+int astro_rollout(const AstroParams *p, const AstroState *s, const AstroPolicy *policy, int32_t ticks,
+                  const int8_t *control, float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset,
+                  void *stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if ((rc = check_state(s))) return rc;
+    if (!policy) return fail(-70, "policy is NULL");
+    if (policy->kind < ASTRO_POLICY_CONTROL || policy->kind > ASTRO_POLICY_RANDOM)
+        return fail(-71, "policy kind must be CONTROL, NOTHING or RANDOM");
+    if (ticks < 1) return fail(-72, "ticks must be >= 1");
+    if (s->n_env == 0) return 0;
+    if (policy->kind == ASTRO_POLICY_CONTROL && !control) return fail(-73, "policy CONTROL needs control");
+    if (!reward || !done) return fail(-30, "control/reward/done is NULL");
+    if (auto_reset && !s->stream) return fail(-31, "auto_reset needs the stream array");
+    if (p->nships == 2 && ((reinterpret_cast<uintptr_t>(control) & 1u) || (reinterpret_cast<uintptr_t>(reward) & 7u)))
+        return fail(-32, "control must be 2-byte and reward 8-byte aligned");
+    if (int64_t(s->n_env) * 4 > int64_t(0x7fffffff)) return fail(-34, "n_env too large");
+    if (stats && (reinterpret_cast<uintptr_t>(stats) & 7u)) return fail(-33, "stats must be 8-byte aligned");
+    const TickDriver drv{control, policy->kind, ticks, policy->seed, policy->tick0, policy->env_offset};
+    return dispatch<StepL>(*p, *s, drv, reward, done, stats, int(auto_reset), reinterpret_cast<hipStream_t>(stream));
 }
 
 int astro_reset(const AstroParams *p, const AstroState *s, const uint32_t *seeds, const uint8_t *mask,

@@ -209,6 +209,34 @@ class BatchedEnv:
             planets=self.planets.permute(1, 0, 2), nplanets=self.nplanets,
             bullets=self.bullets, nbullets=self.nbullets, tick=self.tick)
 
+    def rollout(self, ticks, policy='random', seed=0, tick0=0, auto_reset=None, stats=True):
+        """``ticks`` consecutive steps with open-loop controls, in one launch
+        (quad kernel; one per tick for the lane kernel): exactly ``ticks``
+        calls of ``step`` with those controls.  ``policy``: 'random'
+        (bench.py's splitmix64 controls keyed by GLOBAL env id and
+        ``tick0 + k``), 'nothing' (script.NothingBot), or an int8 tensor
+        [ticks, N, S] of controls.  Returns (reward [ticks, N, S],
+        done [ticks, N])."""
+        ticks = int(ticks)
+        ar = self.auto_reset if auto_reset is None else bool(auto_reset)
+        ctl = None
+        if torch.is_tensor(policy):
+            ctl = policy.to(device=self.device, dtype=torch.int8).contiguous()
+            if tuple(ctl.shape) != (ticks, self.n_env, self.S):
+                raise ValueError('control must be [%d, %d, %d]' % (ticks, self.n_env, self.S))
+            kind = _lib.POLICIES['control']
+        else:
+            kind = _lib.POLICIES[policy]
+        pol = _lib.AstroPolicy(kind=kind, seed=int(seed), tick0=int(tick0), env_offset=self.env_offset)
+        reward = torch.empty((ticks, self.n_env, self.S), dtype=torch.float32, device=self.device)
+        done = torch.empty((ticks, self.n_env), dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.astro_rollout(
+            ctypes.byref(self.params), ctypes.byref(self.state), ctypes.byref(pol), ticks,
+            None if ctl is None else ctl.data_ptr(), reward.data_ptr(), done.data_ptr(),
+            self.stats.data_ptr() if stats else None, int(ar), _stream_ptr(self.device)), 'astro_rollout')
+        self._keep_rollout = ctl
+        return reward, done
+
     def features(self, rows=None, out=None):
         """Observation features of every env, as rl.ValueNetwork.get_features
         then to_batch (rl.py:36-112): float32 [N, rows, 1 + 5*S + 4], rows

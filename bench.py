@@ -112,6 +112,10 @@ def main():
                     help='launches per captured hipGraph in the timed region (0 = eager launches)')
     ap.add_argument('--calib', type=int, default=100,
                     help='eager launches timed one by one (hipEvent pairs) for the kernel duration')
+    ap.add_argument('--rollout', type=int, default=100,
+                    help='secondary line: the workload as K-tick rollouts with the on-device random '
+                         'policy, K ticks per launch (0 = skip)')
+    ap.add_argument('--no-features', action='store_true', help='skip the observation-builder line')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -201,6 +205,48 @@ def main():
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
+    # Secondary lines (not the headline `value`).  (1) The same workload as
+    # K-tick rollouts: controls from the on-device splitmix64 policy (the
+    # same stream as `controls`), K ticks per launch, each wave stepping its
+    # envs without a grid-wide barrier between ticks -- for open-loop or
+    # scripted control, where no policy needs the observation between ticks.
+    extras = {}
+    if args.rollout > 0:
+        K = args.rollout
+        reps = max(1, args.steps // K)
+        base = ticks + args.calib
+        env.rollout(K, 'random', tick0=base, stats=False)
+        barrier()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tr0 = time.perf_counter()
+        r0.record(stream)
+        for r in range(reps):
+            env.rollout(K, 'random', tick0=base + (r + 1) * K, stats=False)
+        r1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall_r = _shard.max_over_ranks(time.perf_counter() - tr0, device=red_dev)
+        barrier()
+        extras['rollout'] = dict(
+            ticks_per_launch=K, launches=reps, value=n * world * K * reps / wall_r, unit='env-steps/s',
+            ms_per_tick=wall_r / (K * reps) * 1e3, gpu_ms_per_tick=r0.elapsed_time(r1) / (K * reps),
+            policy='on-device splitmix64 random controls (bench controls stream)')
+    # (2) The observation builder (rl.ValueNetwork.get_features + to_batch):
+    # an HBM-write-bound kernel; bytes = the float32 feature tensor written.
+    if not args.no_features:
+        out_f = env.features()
+        torch.cuda.synchronize(dev)
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record(stream)
+        for _ in range(20):
+            env.features(out=out_f)
+        f1.record(stream)
+        torch.cuda.synchronize(dev)
+        fms = f0.elapsed_time(f1) / 20
+        fbytes = out_f.numel() * 4
+        extras['observation'] = dict(
+            kernel='astro_features_kernel', shape=list(out_f.shape), ms=fms,
+            write_GBps=fbytes / (fms * 1e-3) / 1e9, hbm_frac=fbytes / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+
     wall_max = _shard.max_over_ranks(wall, device=red_dev)
     d = {k: s1[k] - s0[k] for k in s0}
     tot = _shard.sum_over_ranks([d[k] for k in ('bullets_in', 'resets', 'overflows', 'collisions',
@@ -247,6 +293,7 @@ def main():
                        collisions=tot[3], timeouts=tot[4],
                        mean_planets=d['planets'] / (n * args.steps)),
         )
+        out.update(extras)
         if world == 1 and not args.no_cpu:
             out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, args.cpu_procs)
             out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']

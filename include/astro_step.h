@@ -7,6 +7,8 @@
  * reference interface, batched over n_env independent games:
  *
  *   astro_step         <- core.step(state, control, config)  core.py:215-303
+ *   astro_rollout      <- core.play's tick loop with Bots.control (core.py:359-410)
+ *                         for open-loop / scripted controls, K ticks per launch
  *                         (plus auto-reset = core.create(next config of the
  *                         env's generate_configs stream), core.py:77-135)
  *   astro_reset        <- core.create(config)                 core.py:86-135
@@ -36,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 6
+#define ASTRO_ABI_VERSION 7
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -100,6 +102,22 @@ typedef struct AstroState {
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
 } AstroState;
 
+/* Control sources of astro_rollout. */
+enum {
+    ASTRO_POLICY_CONTROL = 0,  /* a control array, int8 [ticks][n_env][nships] */
+    ASTRO_POLICY_NOTHING = 1,  /* script.NothingBot (script.py:6-10): every ship 2 */
+    ASTRO_POLICY_RANDOM = 2    /* uniform [0, 6) per ship and tick: splitmix64 of
+                                  (global ship id, tick) -- bench.py's `controls` */
+};
+
+typedef struct AstroPolicy {
+    int32_t kind;          /* ASTRO_POLICY_* */
+    int32_t reserved;
+    uint64_t seed;         /* RANDOM */
+    int64_t tick0;         /* RANDOM: number of the first tick */
+    int64_t env_offset;    /* RANDOM: global id of env 0 (shards) */
+} AstroPolicy;
+
 /* Statistics accumulated by astro_step when `stats` is non-NULL: uint64
  * [ceil(n_env / 16)][ASTRO_NSTATS], one private row per wave64 (a wave covers
  * 64 envs in the LANE kernel, 16 in the QUAD kernel), added to and never
@@ -127,6 +145,16 @@ const char *astro_last_error(void);
 int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
                float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset,
                void *stream);
+
+/* `ticks` consecutive ticks (each exactly astro_step with auto_reset as
+ * given), controls from `policy`: reward float [ticks][n_env][nships], done
+ * uint8 [ticks][n_env].  The QUAD kernel runs all ticks in ONE launch, each
+ * wave stepping its envs on its own (no grid-wide barrier between ticks);
+ * the LANE kernel launches once per tick.  For open-loop control (a policy
+ * that needs no observation between ticks). */
+int astro_rollout(const AstroParams *p, const AstroState *s, const AstroPolicy *policy, int32_t ticks,
+                  const int8_t *control, float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset,
+                  void *stream);
 
 /* core.create for the envs with mask[i] != 0 (mask NULL = all): from
  * seeds[i] when seeds != NULL, else from the next seed of env i's stream. */

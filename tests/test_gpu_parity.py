@@ -406,3 +406,49 @@ def test_features_batched_run_vs_oracle():
     assert env.features(out=out) is out
     with pytest.raises(ValueError):
         env.features(out=torch.empty((n, 27, 15), dtype=torch.float32, device='cuda:0'))
+
+
+# ------------------------------------------------------- K-tick rollouts
+
+@pytest.mark.parametrize('kernel', KERNELS)
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_rollout_equals_stepping(kernel, dtype):
+    """rollout(K, controls) == K calls of step(controls[k]) bit for bit: every
+    state array, reward and done, auto-reset included (the quad kernel runs
+    the K ticks in one launch)."""
+    cfg = CFG['rapid']
+    n, K = 700, 37
+    a = _env(cfg, n, dtype=dtype, b_cap=24, p_pad=4, auto_reset=True, kernel=kernel)
+    b = _env(cfg, n, dtype=dtype, b_cap=24, p_pad=4, auto_reset=True, kernel=kernel)
+    a.reset()
+    b.reset()
+    ctl = torch.from_numpy(np.random.RandomState(3).randint(0, 6, size=(K, n, 2)).astype(np.int8)).cuda()
+    rew, done = a.rollout(K, ctl)
+    for k in range(K):
+        _, r, d = b.step(ctl[k])
+        assert torch.equal(rew[k], r) and torch.equal(done[k], d), k
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert a.stat_dict() == b.stat_dict()
+
+
+@pytest.mark.parametrize('kernel', KERNELS)
+def test_rollout_device_policies(kernel):
+    """The on-device RANDOM policy draws bench.py's controls (global env id,
+    tick); NOTHING is script.NothingBot's constant 2."""
+    import bench
+    cfg = CFG['default']
+    n, K, off = 513, 12, 1000
+    from astro_amd import BatchedEnv
+    a = BatchedEnv(cfg, n, device='cuda:0', b_cap=32, env_offset=off, kernel=kernel)
+    b = BatchedEnv(cfg, n, device='cuda:0', b_cap=32, env_offset=off, kernel=kernel)
+    a.reset()
+    b.reset()
+    rew, done = a.rollout(K, 'random', seed=0, tick0=5)
+    host = torch.from_numpy(bench.controls(off, n, 2, 5 + K)[5:]).cuda()
+    rew_b, done_b = b.rollout(K, host)
+    assert torch.equal(rew, rew_b) and torch.equal(done, done_b)
+    assert torch.equal(a.ships, b.ships) and torch.equal(a.bullets, b.bullets)
+    rew, done = a.rollout(K, 'nothing')
+    rew_b, done_b = b.rollout(K, torch.full((K, n, 2), 2, dtype=torch.int8, device='cuda:0'))
+    assert torch.equal(rew, rew_b) and torch.equal(done, done_b) and torch.equal(a.planets, b.planets)

@@ -32,7 +32,7 @@ def _declared_functions():
 def test_library_exports_every_header_symbol(lib):
     names = _declared_functions()
     assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_reset',
-                          'astro_stream_init', 'astro_keytable_build', 'astro_features'}
+                          'astro_stream_init', 'astro_keytable_build', 'astro_features', 'astro_rollout'}
     out = subprocess.check_output(['nm', '-D', '--defined-only', _lib.LIB_PATH], text=True)
     exported = set(re.findall(r' T (astro_\w+)$', out, re.M))
     assert set(names) <= exported
@@ -46,7 +46,7 @@ def test_ctypes_struct_layout_matches_header():
     the ctypes mirrors'."""
     lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "astro_step.h"', 'int main(void){']
     expect = []
-    for st in (_lib.AstroParams, _lib.AstroState):
+    for st in (_lib.AstroParams, _lib.AstroState, _lib.AstroPolicy):
         lines.append('printf("%%zu\\n", sizeof(%s));' % st.__name__)
         expect.append(ctypes.sizeof(st))
         for f, _ in st._fields_:
@@ -82,6 +82,13 @@ def test_argument_validation_without_gpu(lib):
     assert lib.astro_features(ctypes.byref(p), ctypes.byref(s), None, 0, None) == 0   # empty batch
     s.n_env = 4
     assert lib.astro_features(ctypes.byref(p), ctypes.byref(s), None, 36, None) == -4  # arrays NULL
+    pol = _lib.AstroPolicy(kind=3)
+    s.n_env = 0
+    assert lib.astro_rollout(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), 4, None, None, None,
+                             None, 0, None) == -71
+    pol.kind = 2
+    assert lib.astro_rollout(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), 0, None, None, None,
+                             None, 0, None) == -72
     assert lib.astro_keytable_build(None, 0, 16, None) == -50
     assert lib.astro_keytable_build(ctypes.c_void_p(16), (1 << 30) - 8, 16, None) == -51
 
