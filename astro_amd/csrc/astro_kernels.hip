@@ -1323,11 +1323,25 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     return todo;
 }
 
-template <typename T, int S, int PMAX, bool MULTI>
-__global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
-                                                                float *__restrict__ reward_all,
-                                                                uint8_t *__restrict__ done_all,
-                                                                unsigned long long *stats, int auto_reset) {
+// Counters one tick of a quad-kernel wave adds to its stats row.
+struct QuadCounts {
+    uint32_t n_bin, n_bout, n_pl, n_drop;   // per lane
+    uint32_t c_reset, c_coll, c_tout;       // per wave
+};
+
+#ifdef ASTRO_STAMPS
+#define STAMP_ARG , unsigned long long *stamp_
+#define STAMP_PASS , stamp_
+#else
+#define STAMP_ARG
+#define STAMP_PASS
+#endif
+
+// One tick of the quad kernel's wave (16 envs), tick kt of the launch.
+template <typename T, int S, int PMAX, bool OPAQUE = false>
+__device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
+                                                float *__restrict__ reward_all, uint8_t *__restrict__ done_all,
+                                                bool stats, int auto_reset, int kt STAMP_ARG) {
     using V = typename Store<T>::V;
     constexpr int PPL = PMAX / 4;   // planet slots per lane
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
@@ -1337,7 +1351,8 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     __shared__ uint32_t s_chain[4][2][13 + 2 * S];      // init-key chains of a reset pass, see below
 
     const int N = st.n_env;
-    const int lane = threadIdx.x & 63;
+    int lane = threadIdx.x & 63;
+    if constexpr (OPAQUE) asm volatile("" : "+v"(lane));   // (see the rollout kernel)
     const int q = lane & 3;
     const int e = lane >> 2;
     const int base = blockIdx.x * QENV;
@@ -1351,14 +1366,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     V *bullets = reinterpret_cast<V *>(st.bullets);
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;   // per lane, summed over the launch's ticks
     uint32_t c_reset = 0, c_coll = 0, c_tout = 0;           // per wave
-#ifdef ASTRO_STAMPS
-    unsigned long long stamp_[NSTAMP] = {};
-#endif
     const int sq = q < S ? q : 0;
-    // ---- the launch's ticks: each wave steps its 16 envs on its own, no
-    //      grid-wide barrier between ticks (envs never interact)
-    const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
-    for (int kt = 0; kt < n_ticks; ++kt) {
     float *__restrict__ reward = reward_all + size_t(kt) * NN * S;
     uint8_t *__restrict__ done_out = done_all + size_t(kt) * NN;
     bool f_reset = false, f_coll = false, f_tout = false;
@@ -1811,39 +1819,85 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
         stamp_[15] = n_res | (n_t0 << 8) | ((unsigned long long)total << 16);
     }
 #endif
-    if (kt + 1 < n_ticks) __syncthreads();   // this tick's stores are seen by the wave's next
-    }   // ticks
-    STAMP(11);
+    return QuadCounts{n_bin, n_bout, n_pl, n_drop, c_reset, c_coll, c_tout};
+}
+
+// Add one tick's counters to the wave's private stats row (lane 0).  A
+// lane's per-tick counts are < 2^16 and, for b_cap < 4,096, so are their
+// sums over the wave's 16 envs: two counters then share one wave sum.
+__device__ __forceinline__ void flush_counts(unsigned long long *slot, const QuadCounts &c, bool packed) {
+    const uint32_t a = wave_sum32(packed ? (c.n_bin | (c.n_bout << 16)) : c.n_bin);
+    const uint32_t b = wave_sum32(packed ? (c.n_pl | (c.n_drop << 16)) : c.n_bout);
+    const uint32_t x = packed ? 0u : wave_sum32(c.n_pl);
+    const uint32_t y = packed ? 0u : wave_sum32(c.n_drop);
+    if ((threadIdx.x & 63) == 0) {
+        const uint64_t bin = packed ? (a & 0xffff) : a;
+        const uint64_t bout = packed ? (a >> 16) : b;
+        const uint64_t pl = packed ? (b & 0xffff) : x;
+        const uint64_t drop = packed ? (b >> 16) : y;
+        if (bin) atomicAdd(slot + ASTRO_STAT_BULLETS_IN, (unsigned long long)bin);
+        if (bout) atomicAdd(slot + ASTRO_STAT_BULLETS_OUT, (unsigned long long)bout);
+        if (c.c_reset) atomicAdd(slot + ASTRO_STAT_RESETS, (unsigned long long)c.c_reset);
+        if (c.c_coll) atomicAdd(slot + ASTRO_STAT_COLLISIONS, (unsigned long long)c.c_coll);
+        if (c.c_tout) atomicAdd(slot + ASTRO_STAT_TIMEOUTS, (unsigned long long)c.c_tout);
+        if (drop) atomicAdd(slot + ASTRO_STAT_OVERFLOWS, (unsigned long long)drop);
+        if (pl) atomicAdd(slot + ASTRO_STAT_PLANETS, (unsigned long long)pl);
+    }
+}
+
+// astro_rollout's quad kernel takes its arguments as ONE struct, so the
+// tick function can read them straight from the kernarg segment (scalar
+// loads) instead of from a private copy.
+struct QuadArgs {
+    AstroParams p;
+    AstroState st;
+    TickDriver drv;
+    float *reward;
+    uint8_t *done;
+    unsigned long long *stats;
+    int auto_reset;
+};
+typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
+
+
+template <typename T, int S, int PMAX, bool MULTI>
+__global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+                                                                float *__restrict__ reward_all,
+                                                                uint8_t *__restrict__ done_all,
+                                                                unsigned long long *stats, int auto_reset) {
 #ifdef ASTRO_STAMPS
-    if (stats && lane == 0) {
+    unsigned long long stamp_[NSTAMP] = {};
+    quad_tick<T, S, PMAX>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0, stamp_);
+    STAMP(11);
+    if (stats && (threadIdx.x & 63) == 0) {
         unsigned long long *row = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * NSTAMP;
         for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
     }
-    return;
-#endif
-
-    if (stats) {   // one private row per wave (16 envs)
-        // per-lane counts and their wave sums fit 16 bits when b_cap * ticks * 16 < 2^16
-        const bool packed = uint64_t(p.b_cap) * uint64_t(n_ticks) * 16u < 65536u;
-        const uint32_t a = wave_sum32(packed ? (n_bin | (n_bout << 16)) : n_bin);
-        const uint32_t b = wave_sum32(packed ? (n_pl | (n_drop << 16)) : n_bout);
-        const uint32_t c = packed ? 0u : wave_sum32(n_pl);
-        const uint32_t d = packed ? 0u : wave_sum32(n_drop);
-        if (lane == 0) {
-            unsigned long long *slot = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * ASTRO_NSTATS;
-            const uint64_t bin = packed ? (a & 0xffff) : a;
-            const uint64_t bout = packed ? (a >> 16) : b;
-            const uint64_t pl = packed ? (b & 0xffff) : c;
-            const uint64_t drop = packed ? (b >> 16) : d;
-            if (bin) atomicAdd(slot + ASTRO_STAT_BULLETS_IN, (unsigned long long)bin);
-            if (bout) atomicAdd(slot + ASTRO_STAT_BULLETS_OUT, (unsigned long long)bout);
-            if (c_reset) atomicAdd(slot + ASTRO_STAT_RESETS, (unsigned long long)c_reset);
-            if (c_coll) atomicAdd(slot + ASTRO_STAT_COLLISIONS, (unsigned long long)c_coll);
-            if (c_tout) atomicAdd(slot + ASTRO_STAT_TIMEOUTS, (unsigned long long)c_tout);
-            if (drop) atomicAdd(slot + ASTRO_STAT_OVERFLOWS, (unsigned long long)drop);
-            if (pl) atomicAdd(slot + ASTRO_STAT_PLANETS, (unsigned long long)pl);
+#else
+    // ---- the launch's ticks: each wave steps its 16 envs on its own, no
+    //      grid-wide barrier between ticks (envs never interact); the
+    //      counters go to the wave's stats row after every tick, so nothing
+    //      but the tick number lives across the loop
+    const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
+    for (int kt = 0; kt < n_ticks; ++kt) {
+        QuadCounts c;
+        if constexpr (MULTI) {
+            // the arguments through an opaque copy of the kernarg pointer:
+            // scalar loads re-issued each tick instead of hoisted out of the
+            // loop and held across it (which spilled ~120 VGPRs)
+            auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(kp));
+            const QuadArgs &a = *(const QuadArgs *)(KernArgs(kp));
+            c = quad_tick<T, S, PMAX, true>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr, a.auto_reset, kt);
+        } else {
+            c = quad_tick<T, S, PMAX>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, kt);
         }
+        if (stats)
+            flush_counts(stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * ASTRO_NSTATS, c,
+                         p.b_cap < 4096);
+        if (kt + 1 < n_ticks) __syncthreads();   // this tick's stores are seen by the wave's next
     }
+#endif
 }
 
 // ---------------------------------------------------------------------------
