@@ -1113,7 +1113,30 @@ __device__ __forceinline__ bool quad_any(bool f, int lane) {
     return ((__ballot(f) >> (lane & ~3)) & 0xfull) != 0;
 }
 
-constexpr int QENV = BLOCK / 4;   // envs per wave in the quad kernel
+constexpr int QENV = 16;          // envs per wave in the quad kernel
+#ifndef ASTRO_QUAD_WAVES
+#define ASTRO_QUAD_WAVES 4
+#endif
+// Waves per quad-kernel workgroup.  The waves of a workgroup share nothing
+// (each has its own LDS rows and syncs only itself); four per workgroup make
+// a quarter as many workgroups for the dispatcher (launch floor 2.0 -> 1.6
+// us, tools/mb_launch.hip).
+constexpr int QW = ASTRO_QUAD_WAVES;
+constexpr int QBLOCK = 64 * QW;
+
+// A wave's own LDS traffic in order: every lane's writes before any lane's
+// later reads (LDS runs a wave's instructions in issue order; this keeps the
+// compiler from reordering around it).  No s_barrier: waves never wait for
+// each other.
+__device__ __forceinline__ void wave_sync() {
+    if constexpr (QW == 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
 constexpr int QWIN = 1024;        // live bullets per window of the quad kernel's LDS index
 
 // Inclusive prefix sum over the 64 lanes of a wave (all lanes active): DPP
@@ -1264,10 +1287,10 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
 #pragma unroll
         for (int k = 0; k <= NW; ++k) s_chain[row][u][k] = xs[k];
     }
-    __syncthreads();
+    wave_sync();
     const int uw = u < NW ? u : 0;
     const uint32_t a0 = s_chain[row][0][uw], a1 = s_chain[row][0][uw + 1], b0 = s_chain[row][1][uw];
-    __syncthreads();   // s_chain is free for the next pass
+    wave_sync();   // s_chain is free for the next pass
     const uint32_t y = (a0 & 0x80000000u) | (a1 & 0x7fffffffu);
     const uint32_t w = mt_temper(b0 ^ (y >> 1) ^ ((a1 & 1u) ? 0x9908b0dfu : 0u));   // output u
 
@@ -1345,17 +1368,23 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     using V = typename Store<T>::V;
     constexpr int PPL = PMAX / 4;   // planet slots per lane
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
-    __shared__ float4 s_body[QENV][NBOD2];              // float32 (x, y): ships, then planets (padding far)
-    __shared__ uint32_t s_index[QWIN];   // a window of the wave's live bullets, see bw_*
-    __shared__ int s_kept[QENV], s_hit[QENV], s_serial[QENV];
-    __shared__ uint32_t s_chain[4][2][13 + 2 * S];      // init-key chains of a reset pass, see below
+    // LDS, one set per wave of the workgroup
+    __shared__ float4 s_body_all[QW][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
+    __shared__ uint32_t s_index_all[QW][QWIN];           // a window of the wave's live bullets, see bw_*
+    __shared__ int s_kept_all[QW][QENV], s_hit_all[QW][QENV], s_serial_all[QW][QENV];
+    __shared__ uint32_t s_chain_all[QW][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
+    const int wv = QW == 1 ? 0 : int(threadIdx.x >> 6);
+    float4 (*s_body)[NBOD2] = s_body_all[wv];
+    uint32_t *s_index = s_index_all[wv];
+    int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv];
+    uint32_t (*s_chain)[2][13 + 2 * S] = s_chain_all[wv];
 
     const int N = st.n_env;
     int lane = threadIdx.x & 63;
     if constexpr (OPAQUE) asm volatile("" : "+v"(lane));   // (see the rollout kernel)
     const int q = lane & 3;
     const int e = lane >> 2;
-    const int base = blockIdx.x * QENV;
+    const int base = (blockIdx.x * QW + wv) * QENV;
     const bool active = base + e < N;     // uniform over the quad
     const int i = active ? base + e : N - 1;   // spare quads of the last wave shadow env N-1, store nothing
     const size_t NN = size_t(N);
@@ -1401,7 +1430,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     STAMP(1);
     const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
     uint32_t pend_key = uint32_t(h.w);
-    if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
     n_pl += active && q == 0 ? uint32_t(np) : 0u;
 
     // ---- index the wave's live bullets densely: bullet k of env e is number
@@ -1421,12 +1449,16 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         s_hit[e] = 0;
         s_serial[e] = 0;
     }
-    __syncthreads();
+    wave_sync();
     // the first two rounds' bullets load during the physics below
     uint32_t bw0 = lane < total ? s_index[lane] : 0u;
     uint32_t bw1 = lane + 64 < min(total, QWIN) ? s_index[lane + 64] : 0u;
     V cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
     V cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
+    // key[397] of the next game's seed (first step of a game): a random
+    // gather into the 4 GiB key table, issued after every load the physics
+    // waits for, so only its consumers (header store, reset) wait for it
+    if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
 
     // ---- quad broadcasts: all planets, both ships
     double px[PMAX], py[PMAX], sx[S], sy[S];
@@ -1526,7 +1558,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #pragma unroll
         for (int m = 0; m < PPL; ++m) body[S + q + 4 * m] = make_float2(mpxf[m], mpyf[m]);
     }
-    __syncthreads();
+    wave_sync();
 
     STAMP(3);
     // ---- bullets (core.py:241-251, 264-266, 295-300): lane g of a round
@@ -1542,9 +1574,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         for (int w0 = 0; w0 < total; w0 += QWIN) {   // uniform; one window unless > 64 bullets/env
           const int wend = min(total, w0 + QWIN);
           if (w0 > 0) {
-              __syncthreads();   // the previous window is read
+              wave_sync();   // the previous window is read
               index_window(s_index, w0, off, nb, q, tag);
-              __syncthreads();
+              wave_sync();
               bw0 = w0 + lane < wend ? s_index[lane] : 0u;
               bw1 = w0 + 64 + lane < wend ? s_index[64 + lane] : 0u;
               cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
@@ -1650,9 +1682,14 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
           }
         }
     }
-    __syncthreads();
+    wave_sync();
     const int wr_in = s_kept[e];
     const int hit_bits = s_hit[e];
+    // the stores below recompute their addresses from an opaque copy of the
+    // env index (holding the load addresses live across the bullet pass
+    // costs registers the bullet pass needs)
+    int is = i;
+    asm volatile("" : "+v"(is));
     n_bin += active && q == 0 ? uint32_t(nb) : 0u;
     STAMP(4);
 
@@ -1665,9 +1702,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         const uint8_t done = collided ? 1 : (timeout ? 2 : 0);
         if (q < S) {   // rewards (core.py:253-260): lane s writes ship s's
             const bool mh = q == 0 ? hit[0] : hit[S - 1];
-            reward[size_t(i) * S + q] = collided ? (mh ? -1.0f : 1.0f) : (timeout ? p.timeout_reward : 0.0f);
+            reward[size_t(is) * S + q] = collided ? (mh ? -1.0f : 1.0f) : (timeout ? p.timeout_reward : 0.0f);
         }
-        if (q == 0) done_out[i] = done;
+        if (q == 0) done_out[is] = done;
         STAMP(5);
 
         if (!done) {   // uniform over the quad
@@ -1702,7 +1739,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 }
                 const uint64_t nib = (__ballot(keep) >> (lane & ~3)) & 0xfull;
                 const int pos = wr + __popcll(nib & ((1ull << q) - 1));
-                if (keep && pos < p.b_cap) bullets[size_t(i) * BC + pos] = out;
+                if (keep && pos < p.b_cap) bullets[size_t(is) * BC + pos] = out;
                 wr += __popcll(nib);
             }
             const int w = wr < p.b_cap ? wr : p.b_cap;
@@ -1717,14 +1754,32 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 v.y = T(wrap_unit<double>(my + p.dt * ndy));
                 v.z = T(ndx);
                 v.w = T(ndy);
-                ships[size_t(q) * NN + i] = v;
-                ships_b[size_t(q) * NN + i] = T(mb + p.db * double((ctl >> 1) - 1));
+                ships[size_t(q) * NN + is] = v;
+                ships_b[size_t(q) * NN + is] = T(mb + p.db * double((ctl >> 1) - 1));
             }
 
             STAMP(6);
             // ---- own planets: gravity of all planets incl. self, in order
             //      (core.py:289-294); float32 at tick 0 / for a lone planet
             const float dtf = float(p.dt);
+            {   // the planets again from the quad (DPP) rather than 2*PMAX
+                // doubles held live across the bullet pass
+                T rx[PPL], ry[PPL];
+#pragma unroll
+                for (int m = 0; m < PPL; ++m) {
+                    rx[m] = mpx[m];
+                    ry[m] = mpy[m];
+                    asm volatile("" : "+v"(rx[m]), "+v"(ry[m]));
+                }
+                bcast_slots<T, 0, PPL>(rx, px);
+                bcast_slots<T, 1, PPL>(rx, px);
+                bcast_slots<T, 2, PPL>(rx, px);
+                bcast_slots<T, 3, PPL>(rx, px);
+                bcast_slots<T, 0, PPL>(ry, py);
+                bcast_slots<T, 1, PPL>(ry, py);
+                bcast_slots<T, 2, PPL>(ry, py);
+                bcast_slots<T, 3, PPL>(ry, py);
+            }
 #pragma unroll
             for (int m = 0; m < PPL; ++m) {
                 const int j = q + 4 * m;
@@ -1764,7 +1819,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                         v.z = T(ndx);
                         v.w = T(ndy);
                     }
-                    planets[size_t(j) * NN + i] = v;
+                    planets[size_t(j) * NN + is] = v;
                 }
             }
 
@@ -1772,7 +1827,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             if (q == 0) {
                 const int fl = flags | (dropped ? 1 : 0);
                 const uint32_t kv = (key_valid || p.key_table) ? KEY_VALID : 0u;
-                reinterpret_cast<int4 *>(st.hdr)[i] =
+                reinterpret_cast<int4 *>(st.hdr)[is] =
                     make_int4(int(uint32_t(tick + 1) | kv), np | (fl << 8) | (w << 16), int(pend_seed), int(pend_key));
                 n_bout += uint32_t(w);
                 n_drop += uint32_t(dropped);
@@ -1791,15 +1846,15 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     //      up to four per pass with 16 lanes each (wave_reset_pass); rejected
     //      randint words (max_planets not a power of two) take the serial path
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
-        todo = wave_reset_pass<T, S, PMAX>(p, st, todo, lane, i, pend_seed, pend_key, key_valid || p.key_table,
+        todo = wave_reset_pass<T, S, PMAX>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
                                            s_chain, s_serial);
     if (auto_reset) {
-        __syncthreads();
+        wave_sync();
         if (active && s_serial[e]) {   // uniform over the quad; rare
             const uint32_t kq = uint32_t(quad_bcast_i<0>(int(pend_key)));   // lane q == 0 fetched it
-            const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+            const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
             const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, c.x, c.y, c.z);
-            restart_env<T, S, PMAX, 4>(p, st, i, pend_seed, ng, q);
+            restart_env<T, S, PMAX, 4>(p, st, is, pend_seed, ng, q);
         }
     }
     STAMP(10);
@@ -1861,7 +1916,7 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 
 template <typename T, int S, int PMAX, bool MULTI>
-__global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+__global__ __launch_bounds__(QBLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {
@@ -1870,7 +1925,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     quad_tick<T, S, PMAX>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0, stamp_);
     STAMP(11);
     if (stats && (threadIdx.x & 63) == 0) {
-        unsigned long long *row = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * NSTAMP;
+        unsigned long long *row = stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * NSTAMP;
         for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
     }
 #else
@@ -1878,6 +1933,7 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
     //      grid-wide barrier between ticks (envs never interact); the
     //      counters go to the wave's stats row after every tick, so nothing
     //      but the tick number lives across the loop
+    if (int(blockIdx.x * QW + threadIdx.x / 64) * QENV >= st.n_env) return;   // a spare wave of the last block
     const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
     for (int kt = 0; kt < n_ticks; ++kt) {
         QuadCounts c;
@@ -1893,9 +1949,11 @@ __global__ __launch_bounds__(BLOCK, 4) void astro_step_quad_kernel(AstroParams p
             c = quad_tick<T, S, PMAX>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, kt);
         }
         if (stats)
-            flush_counts(stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * ASTRO_NSTATS, c,
+            flush_counts(stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * ASTRO_NSTATS, c,
                          p.b_cap < 4096);
-        if (kt + 1 < n_ticks) __syncthreads();   // this tick's stores are seen by the wave's next
+        // this tick's stores (other lanes' bullets included) before the
+        // wave's next tick reads them: vmcnt(0), on this CU's own L1
+        if (kt + 1 < n_ticks) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
 #endif
 }
@@ -2080,12 +2138,12 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
                 uint64_t *stats, int ar, hipStream_t stream) {
     unsigned long long *st = reinterpret_cast<unsigned long long *>(stats);
     if (pick_kernel(p, s.n_env) == ASTRO_KERNEL_QUAD) {   // all ticks in one launch
-        const int grid = int((int64_t(s.n_env) * 4 + BLOCK - 1) / BLOCK);
+        const int grid = int((int64_t(s.n_env) * 4 + QBLOCK - 1) / QBLOCK);
         if (drv.ticks == 1)
-            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false>), dim3(grid), dim3(BLOCK), 0, stream, p, s,
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false>), dim3(grid), dim3(QBLOCK), 0, stream, p, s,
                                drv, r, d, st, ar);
         else
-            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true>), dim3(grid), dim3(BLOCK), 0, stream, p, s,
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true>), dim3(grid), dim3(QBLOCK), 0, stream, p, s,
                                drv, r, d, st, ar);
         return launched("astro_step(quad)");
     }

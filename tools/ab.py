@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""A/B timing of library builds on the bench's own timed region (hipGraph
+replays of 100 astro_step launches, c3 by default), interleaved over rounds
+so clock drift hits every build alike.
+
+    python tools/ab.py --libs libastro_hip,libastro_hip_var [--workload c3] [--rounds 5]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from astro_amd import BatchedEnv, DEFAULT_CONFIG, _lib  # noqa: E402
+
+
+def make(lib, wl, n, ticks, rollout):
+    _lib._lib = None
+    _lib.load(os.path.join(ROOT, 'astro_amd', lib + '.so'))
+    w = bench.WORKLOADS[wl]
+    env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=w['b_cap'],
+                     p_pad=w['p_pad'], auto_reset=True)
+    env.reset()
+    ctl = torch.from_numpy(bench.controls(0, n, env.S, ticks)).cuda()
+    for t in range(50):
+        env.launch(ctl[t].data_ptr())
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for t in range(50, 150):
+                env.launch(ctl[t].data_ptr())
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    return env, g
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--libs', required=True)
+    ap.add_argument('--workload', default='c3')
+    ap.add_argument('--n-env', type=int, default=0)
+    ap.add_argument('--rounds', type=int, default=5)
+    ap.add_argument('--reps', type=int, default=5)
+    a = ap.parse_args()
+    libs = a.libs.split(',')
+    n = a.n_env or bench.WORKLOADS[a.workload]['n']
+    res = {l: [] for l in libs}
+    rolls = {l: [] for l in libs}
+    for r in range(a.rounds):
+        for lib in libs:
+            env, g = make(lib, a.workload, n, 150, 0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            res[lib].append(e0.elapsed_time(e1) * 1e3 / (100 * a.reps))
+            e0.record()
+            env.rollout(100, 'random', tick0=1000, stats=False)
+            e1.record()
+            torch.cuda.synchronize()
+            rolls[lib].append(e0.elapsed_time(e1) * 1e3 / 100)
+            del g, env
+    for lib in libs:
+        v = np.array(res[lib])
+        print(json.dumps(dict(lib=lib, workload=a.workload, n=n, us_per_launch_median=float(np.median(v)),
+                              us_all=[round(x, 3) for x in v],
+                              rollout_us_per_tick=float(np.median(rolls[lib])))), flush=True)
+
+
+if __name__ == '__main__':
+    main()
