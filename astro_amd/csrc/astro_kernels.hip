@@ -2128,8 +2128,15 @@ int launched(const char *what) {
 // kernel choice: the quad kernel fills the chip with 4 waves per SIMD where a
 // lane per env would leave it at <= 2 (fewer than 2 x 64 x 1024 envs); past
 // that the lane-per-env kernel has the occupancy and fewer instructions
+// AUTO: measured on MI355X (profiles/round1/kernel_choice.jsonl, bench.py's
+// timed region): the quad kernel wins up to 262,144 envs with 4 planet slots
+// and at every measured size with 8 (1.6x at 131,072: the lane kernel's
+// serial 8-planet loops), the lane kernel at 1M envs with 4; 16 slots spill
+// the quad kernel's registers.
 int pick_kernel(const AstroParams &p, int n_env) {
     if (p.kernel == ASTRO_KERNEL_LANE || p.kernel == ASTRO_KERNEL_QUAD) return p.kernel;
+    if (p.p_pad > 8) return ASTRO_KERNEL_LANE;
+    if (p.p_pad > 4) return ASTRO_KERNEL_QUAD;
     return n_env <= ASTRO_QUAD_MAX_ENVS ? ASTRO_KERNEL_QUAD : ASTRO_KERNEL_LANE;
 }
 

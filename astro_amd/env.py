@@ -64,6 +64,9 @@ def key_table(device):
     return t
 
 
+QUAD_MAX_ENVS = 262144   # include/astro_step.h ASTRO_QUAD_MAX_ENVS
+
+
 class BatchedEnv:
     """N lockstep games of one Config on one device.
 
@@ -178,6 +181,19 @@ class BatchedEnv:
             stream if stream is not None else _stream_ptr(self.device))
         if rc != 0:
             _lib.check(rc, 'astro_step')
+
+    @property
+    def step_kernel(self):
+        """'quad' or 'lane': the kernel astro_step runs for this env batch
+        (the library's AUTO rule, pick_kernel in astro_kernels.hip)."""
+        k = self.params.kernel
+        if k in (_lib.KERNELS['lane'], _lib.KERNELS['quad']):
+            return 'lane' if k == _lib.KERNELS['lane'] else 'quad'
+        if self.p_pad > 8:
+            return 'lane'
+        if self.p_pad > 4:
+            return 'quad'
+        return 'quad' if self.n_env <= QUAD_MAX_ENVS else 'lane'
 
     # ------------------------------------------------------------ observation
 

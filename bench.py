@@ -282,8 +282,7 @@ def main():
                           frac=achieved / HBM_PEAK_GBS, traffic=traffic,
                           bytes_per_launch=bytes_launch, kernel_ms=launch_ms,
                           kernel_ms_eager_event_pairs=kern_ms,
-                          kernel=('astro_step_quad_kernel' if env.params.kernel == 2 or (
-                              env.params.kernel == 0 and n <= 65536) else 'astro_step_kernel'),
+                          kernel=('astro_step_quad_kernel' if env.step_kernel == 'quad' else 'astro_step_kernel'),
                           timing='hipEvent pair around the timed region / K launches'),
             gpu_ms_per_step=gpu_ms_per_step,
             timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph

@@ -76,11 +76,11 @@ typedef struct AstroParams {
 
 /* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:
  * four lanes per env (16 envs per wave) for ships and planets, and the wave's
- * live bullets spread densely over its 64 lanes; for batches too small to
- * give each SIMD several waves.  AUTO picks QUAD for n_env <=
- * ASTRO_QUAD_MAX_ENVS.  Both give identical results. */
+ * live bullets spread densely over its 64 lanes.  AUTO picks QUAD for
+ * p_pad 5..8, LANE for p_pad > 8, and for p_pad <= 4 QUAD when n_env <=
+ * ASTRO_QUAD_MAX_ENVS (measured crossover).  Both give identical results. */
 enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2 };
-#define ASTRO_QUAD_MAX_ENVS 65536
+#define ASTRO_QUAD_MAX_ENVS 262144
 
 /* Per-env state arrays (device pointers).  hdr packs
  *   hdr[4*i+0] = tick (steps since create, < 2^22) | key_valid << 31

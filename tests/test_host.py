@@ -159,3 +159,11 @@ def test_wrap_formula_matches_numpy_remainder():
     m = np.where(m < 0, m + np.float32(2), m).astype(np.float32)
     m = np.where(m == 0, np.float32(0), m).astype(np.float32)
     assert ((m - np.float32(1)).view(np.int32) == (((x32 + 1) % 2) - 1).view(np.int32)).all()
+
+
+def test_kernel_choice_mirrors_header():
+    """BatchedEnv.step_kernel's AUTO rule uses the header's quad/lane crossover."""
+    from astro_amd import env as _env
+    hdr = open(os.path.join(os.path.dirname(__graft_entry__.__file__), 'include', 'astro_step.h')).read()
+    n = int(re.search(r'#define ASTRO_QUAD_MAX_ENVS (\d+)', hdr).group(1))
+    assert _env.QUAD_MAX_ENVS == n

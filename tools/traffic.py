@@ -12,7 +12,8 @@ import sys
 
 def mean_counter(path, name, skip=20):
     v = [float(r['Counter_Value']) for r in csv.DictReader(open(path))
-         if 'astro_step' in r['Kernel_Name'] and r['Counter_Name'] == name]
+         if 'astro_step' in r['Kernel_Name'] and 'Lb1E' not in r['Kernel_Name']   # not rollouts
+         and r['Counter_Name'] == name]
     v = v[skip:]
     return sum(v) / len(v), len(v)
 
@@ -24,7 +25,7 @@ res = dict(n_env=int(n_env), kernel=kernel, launches=[nf, nw],
            fetch_size_kib=fetch, write_size_kib=write,
            hbm_bytes_per_launch=(2 * fetch + write) * 1024,
            note='read = 2 x FETCH_SIZE (gfx950 counts half of wide coalesced reads), write = WRITE_SIZE; '
-                'the 65,536-env working set fits the 256 MiB Infinity Cache, whose hits these '
+                'working sets below 256 MiB fit the Infinity Cache, whose hits these '
                 'memory-side counters include')
 json.dump(res, open(out, 'w'), indent=1)
 print(json.dumps(res))
