@@ -9,12 +9,12 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'reserved')
 NSTATS = 8
-KERNELS = {'auto': 0, 'lane': 1, 'quad': 2}
+KERNELS = {'auto': 0, 'lane': 1, 'quad': 2, 'pair': 3}
 
 
 class AstroParams(ctypes.Structure):

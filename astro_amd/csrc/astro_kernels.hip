@@ -1085,35 +1085,47 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 // keeps the reference's sequential order, so results are bit-identical to
 // the lane-per-env kernel.
 
-template <int J>
+// Lane groups of LPE = 4 (quad kernel) or 2 (pair kernel) lanes per env.
+// Broadcast lane J of the caller's group with DPP quad_perm: (J,J,J,J) for
+// quads, (J,J,J+2,J+2) for the two pairs of a quad.
+template <int J, int LPE = 4>
 __device__ __forceinline__ int quad_bcast_i(int v) {
-    return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xf, 0xf, false);   // quad_perm(J,J,J,J)
+    static_assert(LPE == 4 || LPE == 2, "groups of 4 or 2 lanes");
+    constexpr int sel = LPE == 4 ? J * 0x55 : (J | (J << 2) | ((J + 2) << 4) | ((J + 2) << 6));
+    return __builtin_amdgcn_mov_dpp(v, sel, 0xf, 0xf, false);
 }
-template <int J>
+template <int J, int LPE = 4>
 __device__ __forceinline__ float quad_bcast(float v) {
-    return __int_as_float(quad_bcast_i<J>(__float_as_int(v)));
+    return __int_as_float(quad_bcast_i<J, LPE>(__float_as_int(v)));
 }
-template <int J>
+template <int J, int LPE = 4>
 __device__ __forceinline__ double quad_bcast(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = quad_bcast_i<J>(int(b & 0xffffffffll));
-    const int hi = quad_bcast_i<J>(int(b >> 32));
+    const int lo = quad_bcast_i<J, LPE>(int(b & 0xffffffffll));
+    const int hi = quad_bcast_i<J, LPE>(int(b >> 32));
     return __longlong_as_double((long long)(uint32_t(lo)) | ((long long)hi << 32));
 }
 
-// broadcast slot m of lane J of the quad into out[4*m + J]
-template <typename T, int J, int PPL>
-__device__ __forceinline__ void bcast_slots(const T (&mine)[PPL], double (&out)[4 * PPL]) {
+// broadcast slot m of every lane J of the group into out[LPE*m + J]
+template <typename T, int PPL, int LPE>
+__device__ __forceinline__ void bcast_slots(const T (&mine)[PPL], double (&out)[LPE * PPL]) {
 #pragma unroll
-    for (int m = 0; m < PPL; ++m) out[4 * m + J] = double(quad_bcast<J>(mine[m]));
+    for (int m = 0; m < PPL; ++m) {
+        out[LPE * m + 0] = double(quad_bcast<0, LPE>(mine[m]));
+        out[LPE * m + 1] = double(quad_bcast<1, LPE>(mine[m]));
+        if constexpr (LPE == 4) {
+            out[LPE * m + 2] = double(quad_bcast<2, LPE>(mine[m]));
+            out[LPE * m + 3] = double(quad_bcast<3, LPE>(mine[m]));
+        }
+    }
 }
 
-// OR of a per-lane flag over the lane's quad (all quad lanes must be active)
+// OR of a per-lane flag over the lane's group (all group lanes must be active)
+template <int LPE = 4>
 __device__ __forceinline__ bool quad_any(bool f, int lane) {
-    return ((__ballot(f) >> (lane & ~3)) & 0xfull) != 0;
+    return ((__ballot(f) >> (lane & ~(LPE - 1))) & ((1ull << LPE) - 1)) != 0;
 }
 
-constexpr int QENV = 16;          // envs per wave in the quad kernel
 #ifndef ASTRO_QUAD_WAVES
 #define ASTRO_QUAD_WAVES 4
 #endif
@@ -1153,21 +1165,25 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
     return v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
 }
 
-// Bullet index word (LDS): env in the wave | slot << 4 | last-of-env << 20 |
-// nplanets << 21 | tick-0 << 26
-__device__ __forceinline__ int bw_env(uint32_t w) { return int(w & 15u); }
-__device__ __forceinline__ int bw_slot(uint32_t w) { return int((w >> 4) & 0xffffu); }
-__device__ __forceinline__ bool bw_last(uint32_t w) { return (w >> 20) & 1u; }
-__device__ __forceinline__ int bw_np(uint32_t w) { return int((w >> 21) & 31u); }
-__device__ __forceinline__ bool bw_t0(uint32_t w) { return (w >> 26) & 1u; }
+// Bullet index word (LDS): env in the wave | slot << 5 | last-of-env << 21 |
+// nplanets << 22 | tick-0 << 27
+__device__ __forceinline__ int bw_env(uint32_t w) { return int(w & 31u); }
+__device__ __forceinline__ int bw_slot(uint32_t w) { return int((w >> 5) & 0xffffu); }
+__device__ __forceinline__ bool bw_last(uint32_t w) { return (w >> 21) & 1u; }
+__device__ __forceinline__ int bw_np(uint32_t w) { return int((w >> 22) & 31u); }
+__device__ __forceinline__ bool bw_t0(uint32_t w) { return (w >> 27) & 1u; }
+__device__ __forceinline__ uint32_t bw_tag(int e, int np, bool t0) {
+    return uint32_t(e) | (uint32_t(np) << 22) | (t0 ? 1u << 27 : 0u);
+}
 
-// Index window [w0, w0 + QWIN) of the wave's live bullets: the quad of an
+// Index window [w0, w0 + QWIN) of the wave's live bullets: the group of an
 // env whose bullets are numbered off .. off + nb - 1 writes the words of
-// those in the window, lane q taking slots k = q mod 4.
+// those in the window, lane q taking slots k = q mod LPE.
+template <int LPE>
 __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off, int nb, int q, uint32_t tag) {
     const int lo = max(0, w0 - off), hi = min(nb, w0 + QWIN - off);
-    for (int k = lo + ((q - lo) & 3); k < hi; k += 4)
-        s_index[off + k - w0] = tag | (uint32_t(k) << 4) | (k == nb - 1 ? 1u << 20 : 0u);
+    for (int k = lo + ((q - lo) & (LPE - 1)); k < hi; k += LPE)
+        s_index[off + k - w0] = tag | (uint32_t(k) << 5) | (k == nb - 1 ? 1u << 21 : 0u);
 }
 
 // create() of one env spread over a row of 16 lanes, for PMAX <= 7: each
@@ -1253,7 +1269,7 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
 // then runs spread over the row (ship u, planet u).  An env whose first
 // randint word is rejected is flagged in s_serial for the quad's serial
 // create.  Returns the leaders not yet served.
-template <typename T, int S, int PMAX>
+template <typename T, int S, int PMAX, int LPE>
 __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
                                                     int lane, int i, uint32_t pend_seed, uint32_t pend_key,
                                                     bool have_key, uint32_t (*s_chain)[2][13 + 2 * S],
@@ -1342,7 +1358,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
             reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | ((exhausted || cf) ? 2 << 8 : 0), int(next_seed), 0);
         }
     }
-    if (on && !fast && u == 0) s_serial[L >> 2] = 1;
+    if (on && !fast && u == 0) s_serial[L / LPE] = 1;
     return todo;
 }
 
@@ -1361,12 +1377,13 @@ struct QuadCounts {
 #endif
 
 // One tick of the quad kernel's wave (16 envs), tick kt of the launch.
-template <typename T, int S, int PMAX, bool OPAQUE = false>
+template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false>
 __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
                                                 float *__restrict__ reward_all, uint8_t *__restrict__ done_all,
                                                 bool stats, int auto_reset, int kt STAMP_ARG) {
     using V = typename Store<T>::V;
-    constexpr int PPL = PMAX / 4;   // planet slots per lane
+    constexpr int PPL = PMAX / LPE;   // planet slots per lane
+    constexpr int QENV = 64 / LPE;    // envs per wave
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
     // LDS, one set per wave of the workgroup
     __shared__ float4 s_body_all[QW][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
@@ -1382,8 +1399,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const int N = st.n_env;
     int lane = threadIdx.x & 63;
     if constexpr (OPAQUE) asm volatile("" : "+v"(lane));   // (see the rollout kernel)
-    const int q = lane & 3;
-    const int e = lane >> 2;
+    const int q = lane & (LPE - 1);
+    const int e = lane / LPE;
     const int base = (blockIdx.x * QW + wv) * QENV;
     const bool active = base + e < N;     // uniform over the quad
     const int i = active ? base + e : N - 1;   // spare quads of the last wave shadow env N-1, store nothing
@@ -1413,7 +1430,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     T mpx[PPL], mpy[PPL];
 #pragma unroll
     for (int m = 0; m < PPL; ++m) {
-        const int j = q + 4 * m;
+        const int j = q + LPE * m;
         pv[m] = planets[size_t(j < p.p_pad ? j : 0) * NN + i];
         mpx[m] = pv[m].x;
         mpy[m] = pv[m].y;
@@ -1442,8 +1459,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #else
     const int total = __builtin_amdgcn_readlane(incl, 63);
 #endif
-    const uint32_t tag = uint32_t(e) | (uint32_t(np) << 21) | (t0 ? 1u << 26 : 0u);
-    index_window(s_index, 0, off, nb, q, tag);
+    const uint32_t tag = bw_tag(e, np, t0);
+    index_window<LPE>(s_index, 0, off, nb, q, tag);
     if (q == 0) {
         s_kept[e] = 0;
         s_hit[e] = 0;
@@ -1462,19 +1479,13 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 
     // ---- quad broadcasts: all planets, both ships
     double px[PMAX], py[PMAX], sx[S], sy[S];
-    bcast_slots<T, 0, PPL>(mpx, px);
-    bcast_slots<T, 1, PPL>(mpx, px);
-    bcast_slots<T, 2, PPL>(mpx, px);
-    bcast_slots<T, 3, PPL>(mpx, px);
-    bcast_slots<T, 0, PPL>(mpy, py);
-    bcast_slots<T, 1, PPL>(mpy, py);
-    bcast_slots<T, 2, PPL>(mpy, py);
-    bcast_slots<T, 3, PPL>(mpy, py);
-    sx[0] = double(quad_bcast<0>(sv.x));
-    sy[0] = double(quad_bcast<0>(sv.y));
+    bcast_slots<T, PPL, LPE>(mpx, px);
+    bcast_slots<T, PPL, LPE>(mpy, py);
+    sx[0] = double(quad_bcast<0, LPE>(sv.x));
+    sy[0] = double(quad_bcast<0, LPE>(sv.y));
     if (S == 2) {
-        sx[S - 1] = double(quad_bcast<S - 1>(sv.x));
-        sy[S - 1] = double(quad_bcast<S - 1>(sv.y));
+        sx[S - 1] = double(quad_bcast<S - 1, LPE>(sv.x));
+        sy[S - 1] = double(quad_bcast<S - 1, LPE>(sv.y));
     }
 
     // ---- own ship (lanes < S): direction, thrust + gravity (core.py:234-239)
@@ -1520,8 +1531,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     }
 #pragma unroll
     for (int m = 0; m < PPL; ++m) {
-        mpxf[m] = q + 4 * m < np ? float(mpx[m]) : -FAR_POS;
-        mpyf[m] = q + 4 * m < np ? float(mpy[m]) : -FAR_POS;
+        mpxf[m] = q + LPE * m < np ? float(mpx[m]) : -FAR_POS;
+        mpyf[m] = q + LPE * m < np ? float(mpy[m]) : -FAR_POS;
     }
     bool hsp[S];
     {
@@ -1542,7 +1553,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 bool hs = false;
 #pragma unroll
                 for (int m = 0; m < PPL; ++m)
-                    hs |= (q + 4 * m < np) & closer_exact(sx[s], sy[s], double(mpx[m]), double(mpy[m]), gsp, t0);
+                    hs |= (q + LPE * m < np) & closer_exact(sx[s], sy[s], double(mpx[m]), double(mpy[m]), gsp, t0);
                 hsp[s] = amb ? hs : hsp[s];
             }
             if (S == 2 && q == 0) hh = amb ? closer_exact(sx[0], sy[0], sx[S - 1], sy[S - 1], gss, t0) : hh;
@@ -1556,7 +1567,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         float2 *body = reinterpret_cast<float2 *>(&s_body[e][0]);
         if (q < S) body[q] = make_float2(q == 0 ? sxf[0] : sxf[S - 1], q == 0 ? syf[0] : syf[S - 1]);
 #pragma unroll
-        for (int m = 0; m < PPL; ++m) body[S + q + 4 * m] = make_float2(mpxf[m], mpyf[m]);
+        for (int m = 0; m < PPL; ++m) body[S + q + LPE * m] = make_float2(mpxf[m], mpyf[m]);
     }
     wave_sync();
 
@@ -1575,7 +1586,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
           const int wend = min(total, w0 + QWIN);
           if (w0 > 0) {
               wave_sync();   // the previous window is read
-              index_window(s_index, w0, off, nb, q, tag);
+              index_window<LPE>(s_index, w0, off, nb, q, tag);
               wave_sync();
               bw0 = w0 + lane < wend ? s_index[lane] : 0u;
               bw1 = w0 + 64 + lane < wend ? s_index[64 + lane] : 0u;
@@ -1696,7 +1707,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     if (active) {
         bool hit[S];
 #pragma unroll
-        for (int s = 0; s < S; ++s) hit[s] = quad_any(hsp[s], lane) || ((hit_bits >> s) & 1);
+        for (int s = 0; s < S; ++s) hit[s] = quad_any<LPE>(hsp[s], lane) || ((hit_bits >> s) & 1);
         const bool collided = S == 2 ? (hit[0] || hit[S - 1]) : hit[0];
         const bool timeout = !collided && !live;
         const uint8_t done = collided ? 1 : (timeout ? 2 : 0);
@@ -1737,7 +1748,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                         out.w = T(bdy);
                     }
                 }
-                const uint64_t nib = (__ballot(keep) >> (lane & ~3)) & 0xfull;
+                const uint64_t nib = (__ballot(keep) >> (lane & ~(LPE - 1))) & ((1ull << LPE) - 1);
                 const int pos = wr + __popcll(nib & ((1ull << q) - 1));
                 if (keep && pos < p.b_cap) bullets[size_t(is) * BC + pos] = out;
                 wr += __popcll(nib);
@@ -1771,18 +1782,12 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                     ry[m] = mpy[m];
                     asm volatile("" : "+v"(rx[m]), "+v"(ry[m]));
                 }
-                bcast_slots<T, 0, PPL>(rx, px);
-                bcast_slots<T, 1, PPL>(rx, px);
-                bcast_slots<T, 2, PPL>(rx, px);
-                bcast_slots<T, 3, PPL>(rx, px);
-                bcast_slots<T, 0, PPL>(ry, py);
-                bcast_slots<T, 1, PPL>(ry, py);
-                bcast_slots<T, 2, PPL>(ry, py);
-                bcast_slots<T, 3, PPL>(ry, py);
+                bcast_slots<T, PPL, LPE>(rx, px);
+                bcast_slots<T, PPL, LPE>(ry, py);
             }
 #pragma unroll
             for (int m = 0; m < PPL; ++m) {
-                const int j = q + 4 * m;
+                const int j = q + LPE * m;
                 if (j < np) {
                     const double pxj = double(mpx[m]), pyj = double(mpy[m]);
                     const double pdx = double(pv[m].z), pdy = double(pv[m].w);
@@ -1846,15 +1851,15 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     //      up to four per pass with 16 lanes each (wave_reset_pass); rejected
     //      randint words (max_planets not a power of two) take the serial path
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
-        todo = wave_reset_pass<T, S, PMAX>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
+        todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
                                            s_chain, s_serial);
     if (auto_reset) {
         wave_sync();
         if (active && s_serial[e]) {   // uniform over the quad; rare
-            const uint32_t kq = uint32_t(quad_bcast_i<0>(int(pend_key)));   // lane q == 0 fetched it
+            const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(pend_key)));   // lane q == 0 fetched it
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
             const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, c.x, c.y, c.z);
-            restart_env<T, S, PMAX, 4>(p, st, is, pend_seed, ng, q);
+            restart_env<T, S, PMAX, LPE>(p, st, is, pend_seed, ng, q);
         }
     }
     STAMP(10);
@@ -1915,14 +1920,14 @@ struct QuadArgs {
 typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 
-template <typename T, int S, int PMAX, bool MULTI>
+template <typename T, int S, int PMAX, bool MULTI, int LPE>
 __global__ __launch_bounds__(QBLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {
 #ifdef ASTRO_STAMPS
     unsigned long long stamp_[NSTAMP] = {};
-    quad_tick<T, S, PMAX>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0, stamp_);
+    quad_tick<T, S, PMAX, LPE>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0, stamp_);
     STAMP(11);
     if (stats && (threadIdx.x & 63) == 0) {
         unsigned long long *row = stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * NSTAMP;
@@ -1933,7 +1938,7 @@ __global__ __launch_bounds__(QBLOCK, 4) void astro_step_quad_kernel(AstroParams 
     //      grid-wide barrier between ticks (envs never interact); the
     //      counters go to the wave's stats row after every tick, so nothing
     //      but the tick number lives across the loop
-    if (int(blockIdx.x * QW + threadIdx.x / 64) * QENV >= st.n_env) return;   // a spare wave of the last block
+    if (int(blockIdx.x * QW + threadIdx.x / 64) * (64 / LPE) >= st.n_env) return;   // a spare wave of the last block
     const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
     for (int kt = 0; kt < n_ticks; ++kt) {
         QuadCounts c;
@@ -1944,9 +1949,9 @@ __global__ __launch_bounds__(QBLOCK, 4) void astro_step_quad_kernel(AstroParams 
             auto kp = __builtin_amdgcn_kernarg_segment_ptr();
             asm volatile("" : "+s"(kp));
             const QuadArgs &a = *(const QuadArgs *)(KernArgs(kp));
-            c = quad_tick<T, S, PMAX, true>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr, a.auto_reset, kt);
+            c = quad_tick<T, S, PMAX, LPE, true>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr, a.auto_reset, kt);
         } else {
-            c = quad_tick<T, S, PMAX>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, kt);
+            c = quad_tick<T, S, PMAX, LPE>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, kt);
         }
         if (stats)
             flush_counts(stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * ASTRO_NSTATS, c,
@@ -2115,7 +2120,7 @@ int check_params(const AstroParams *p) {
     if (p->b_cap < 1 || p->b_cap > 65535) return fail(-15, "b_cap must be in [1, 65535]");
     if (p->timeout_tick < 0 || p->timeout_tick >= int(TICK_MASK)) return fail(-16, "timeout_tick out of [0, 2^22)");
     if (p->timeout_tick > 0 && !p->fire_bits) return fail(-17, "fire_bits is NULL");
-    if (p->kernel < 0 || p->kernel > 2) return fail(-18, "kernel must be 0 (auto), 1 (lane) or 2 (quad)");
+    if (p->kernel < 0 || p->kernel > 3) return fail(-18, "kernel must be 0 (auto), 1 (lane), 2 (quad) or 3 (pair)");
     return 0;
 }
 
@@ -2129,30 +2134,39 @@ int launched(const char *what) {
 // lane per env would leave it at <= 2 (fewer than 2 x 64 x 1024 envs); past
 // that the lane-per-env kernel has the occupancy and fewer instructions
 // AUTO: measured on MI355X (profiles/round1/kernel_choice.jsonl, bench.py's
-// timed region): the quad kernel wins up to 262,144 envs with 4 planet slots
-// and at every measured size with 8 (1.6x at 131,072: the lane kernel's
-// serial 8-planet loops), the lane kernel at 1M envs with 4; 16 slots spill
-// the quad kernel's registers.
+// timed region).  PAIR (2 lanes per env) wins from 65,536 envs up to the
+// largest size measured (1M: 8.6e9 vs 6.8e9 LANE, 6.6e9 QUAD; c5's 8 planet
+// slots: 4.3e9 vs 3.8e9 QUAD, 2.5e9 LANE); below that QUAD's 4 lanes per env
+// give the SIMDs more waves to hide latency with (16,384 envs: 8.7 us vs
+// 10.2 PAIR); 16 planet slots spill both, LANE.
 int pick_kernel(const AstroParams &p, int n_env) {
-    if (p.kernel == ASTRO_KERNEL_LANE || p.kernel == ASTRO_KERNEL_QUAD) return p.kernel;
+    if (p.kernel == ASTRO_KERNEL_LANE || p.kernel == ASTRO_KERNEL_QUAD || p.kernel == ASTRO_KERNEL_PAIR)
+        return p.kernel;
     if (p.p_pad > 8) return ASTRO_KERNEL_LANE;
-    if (p.p_pad > 4) return ASTRO_KERNEL_QUAD;
-    return n_env <= ASTRO_QUAD_MAX_ENVS ? ASTRO_KERNEL_QUAD : ASTRO_KERNEL_LANE;
+    return n_env <= ASTRO_QUAD_MAX_ENVS ? ASTRO_KERNEL_QUAD : ASTRO_KERNEL_PAIR;
 }
 
 template <typename T, int S, int PM>
 int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv, float *r, uint8_t *d,
                 uint64_t *stats, int ar, hipStream_t stream) {
     unsigned long long *st = reinterpret_cast<unsigned long long *>(stats);
-    if (pick_kernel(p, s.n_env) == ASTRO_KERNEL_QUAD) {   // all ticks in one launch
-        const int grid = int((int64_t(s.n_env) * 4 + QBLOCK - 1) / QBLOCK);
-        if (drv.ticks == 1)
-            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false>), dim3(grid), dim3(QBLOCK), 0, stream, p, s,
-                               drv, r, d, st, ar);
+    const int kind = pick_kernel(p, s.n_env);
+    if (kind == ASTRO_KERNEL_QUAD || kind == ASTRO_KERNEL_PAIR) {   // all ticks in one launch
+        const int lpe = kind == ASTRO_KERNEL_QUAD ? 4 : 2;
+        const int grid = int((int64_t(s.n_env) * lpe + QBLOCK - 1) / QBLOCK);
+        if (lpe == 4 && drv.ticks == 1)
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
+                               s, drv, r, d, st, ar);
+        else if (lpe == 4)
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
+                               s, drv, r, d, st, ar);
+        else if (drv.ticks == 1)
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2>), dim3(grid), dim3(QBLOCK), 0, stream, p,
+                               s, drv, r, d, st, ar);
         else
-            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true>), dim3(grid), dim3(QBLOCK), 0, stream, p, s,
-                               drv, r, d, st, ar);
-        return launched("astro_step(quad)");
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 2>), dim3(grid), dim3(QBLOCK), 0, stream, p,
+                               s, drv, r, d, st, ar);
+        return launched(lpe == 4 ? "astro_step(quad)" : "astro_step(pair)");
     }
 #ifdef ASTRO_ENVS_PER_WAVE
     const int grid = (s.n_env + ASTRO_ENVS_PER_WAVE - 1) / ASTRO_ENVS_PER_WAVE;

@@ -64,7 +64,7 @@ def key_table(device):
     return t
 
 
-QUAD_MAX_ENVS = 262144   # include/astro_step.h ASTRO_QUAD_MAX_ENVS
+QUAD_MAX_ENVS = 32768   # include/astro_step.h ASTRO_QUAD_MAX_ENVS
 
 
 class BatchedEnv:
@@ -77,8 +77,8 @@ class BatchedEnv:
     p_pad      -- planet slots per env (default: config.max_planets)
     dtype      -- torch.float32 (default) or torch.float64 state storage
     env_offset -- global id of env 0 (multi-GPU sharding)
-    kernel     -- 'auto', 'lane' (one lane per env) or 'quad' (four lanes
-                  per env); identical results, different speed
+    kernel     -- 'auto', 'lane' (one lane per env), 'quad' (four lanes
+                  per env) or 'pair' (two); identical results, different speed
     use_key_table -- share the device's 4 GiB seeding table (see key_table);
                   False runs every game's 397-step chain inline (same results)
     """
@@ -187,13 +187,12 @@ class BatchedEnv:
         """'quad' or 'lane': the kernel astro_step runs for this env batch
         (the library's AUTO rule, pick_kernel in astro_kernels.hip)."""
         k = self.params.kernel
-        if k in (_lib.KERNELS['lane'], _lib.KERNELS['quad']):
-            return 'lane' if k == _lib.KERNELS['lane'] else 'quad'
+        for name in ('lane', 'quad', 'pair'):
+            if k == _lib.KERNELS[name]:
+                return name
         if self.p_pad > 8:
             return 'lane'
-        if self.p_pad > 4:
-            return 'quad'
-        return 'quad' if self.n_env <= QUAD_MAX_ENVS else 'lane'
+        return 'quad' if self.n_env <= QUAD_MAX_ENVS else 'pair'
 
     # ------------------------------------------------------------ observation
 

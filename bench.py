@@ -107,7 +107,7 @@ def main():
     ap.add_argument('--cpu-procs', type=int, default=1)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--traffic', default='', help='JSON with PMC-measured HBM bytes per launch')
-    ap.add_argument('--kernel', default='auto', choices=['auto', 'lane', 'quad'])
+    ap.add_argument('--kernel', default='auto', choices=['auto', 'lane', 'quad', 'pair'])
     ap.add_argument('--graph', type=int, default=100,
                     help='launches per captured hipGraph in the timed region (0 = eager launches)')
     ap.add_argument('--calib', type=int, default=100,
@@ -282,7 +282,8 @@ def main():
                           frac=achieved / HBM_PEAK_GBS, traffic=traffic,
                           bytes_per_launch=bytes_launch, kernel_ms=launch_ms,
                           kernel_ms_eager_event_pairs=kern_ms,
-                          kernel=('astro_step_quad_kernel' if env.step_kernel == 'quad' else 'astro_step_kernel'),
+                          kernel=('astro_step_kernel' if env.step_kernel == 'lane' else 'astro_step_quad_kernel'),
+                          lanes_per_env=dict(lane=1, quad=4, pair=2)[env.step_kernel],
                           timing='hipEvent pair around the timed region / K launches'),
             gpu_ms_per_step=gpu_ms_per_step,
             timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph

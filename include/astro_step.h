@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 7
+#define ASTRO_ABI_VERSION 8
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -67,7 +67,7 @@ typedef struct AstroParams {
     int32_t b_cap;         /* bullet slots per env, 1..65535 */
     int32_t timeout_tick;  /* first tick k with max_time <= t_k + dt */
     const uint32_t *fire_bits; /* device: bit k = fire on tick k, k < timeout_tick */
-    int32_t kernel;        /* ASTRO_KERNEL_AUTO / _LANE / _QUAD (results are identical) */
+    int32_t kernel;        /* ASTRO_KERNEL_AUTO / _LANE / _QUAD / _PAIR (results are identical) */
     int32_t reserved;
     const uint32_t *key_table; /* device, optional: key[397] of MT19937 init_genrand for
                                   every seed < 2^30 (astro_keytable_build); NULL = the
@@ -76,11 +76,12 @@ typedef struct AstroParams {
 
 /* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:
  * four lanes per env (16 envs per wave) for ships and planets, and the wave's
- * live bullets spread densely over its 64 lanes.  AUTO picks QUAD for
- * p_pad 5..8, LANE for p_pad > 8, and for p_pad <= 4 QUAD when n_env <=
- * ASTRO_QUAD_MAX_ENVS (measured crossover).  Both give identical results. */
-enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2 };
-#define ASTRO_QUAD_MAX_ENVS 262144
+ * live bullets spread densely over its 64 lanes; PAIR: the same with two
+ * lanes per env (32 envs per wave).  AUTO picks LANE for p_pad > 8, else
+ * QUAD for n_env <= ASTRO_QUAD_MAX_ENVS and PAIR above (measured crossover).
+ * All give identical results. */
+enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2, ASTRO_KERNEL_PAIR = 3 };
+#define ASTRO_QUAD_MAX_ENVS 32768
 
 /* Per-env state arrays (device pointers).  hdr packs
  *   hdr[4*i+0] = tick (steps since create, < 2^22) | key_valid << 31

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 CFG = gio.configs()
 
 
-KERNELS = ['lane', 'quad']
+KERNELS = ['lane', 'quad', 'pair']
 
 
 def _env(cfg, n, dtype=torch.float64, b_cap=64, p_pad=8, auto_reset=False, kernel='auto'):
@@ -260,6 +260,9 @@ def test_full_size_determinism_and_shard_invariance():
     b = run(0, n)
     c = run(0, n, kernel='lane')
     d = run(0, n, kernel='quad')
+    e = run(0, n, kernel='pair')
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
+        assert torch.equal(getattr(a, f), getattr(e, f)), f
     for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
         assert torch.equal(getattr(a, f), getattr(c, f)), f
         assert torch.equal(getattr(a, f), getattr(d, f)), f

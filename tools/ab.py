@@ -3,7 +3,7 @@
 replays of 100 astro_step launches, c3 by default), interleaved over rounds
 so clock drift hits every build alike.
 
-    python tools/ab.py --libs libastro_hip,libastro_hip_var [--workload c3] [--rounds 5]
+    python tools/ab.py --libs libastro_hip,libastro_hip_var[:kernel] [--workload c3] [--rounds 5]
 """
 import argparse
 import json
@@ -20,12 +20,13 @@ import bench  # noqa: E402
 from astro_amd import BatchedEnv, DEFAULT_CONFIG, _lib  # noqa: E402
 
 
-def make(lib, wl, n, ticks, rollout):
+def make(spec, wl, n, ticks, rollout):
+    lib, _, kernel = spec.partition(':')
     _lib._lib = None
     _lib.load(os.path.join(ROOT, 'astro_amd', lib + '.so'))
     w = bench.WORKLOADS[wl]
     env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=w['b_cap'],
-                     p_pad=w['p_pad'], auto_reset=True)
+                     p_pad=w['p_pad'], auto_reset=True, kernel=kernel or 'auto')
     env.reset()
     ctl = torch.from_numpy(bench.controls(0, n, env.S, ticks)).cuda()
     for t in range(50):
