@@ -1593,103 +1593,116 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
               cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
               cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
           }
-          for (int r0 = w0; r0 < wend; r0 += 64) {   // uniform
-            const uint32_t bw = bw0;
-            const V cur = cur0;
-            bw0 = bw1;
-            cur0 = cur1;
-            if (r0 + 128 < wend) {   // prefetch two rounds ahead
-                bw1 = r0 + 128 + lane < wend ? s_index[r0 + 128 + lane - w0] : 0u;
-                cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
-            }
-            const bool valid = r0 + lane < total;
-            const int be = bw_env(bw), bk = bw_slot(bw);
-            const bool bt0 = bw_t0(bw);
-            float bx[2 * NBOD2], by[2 * NBOD2];
+          // one round: lane g takes live bullet r0 + g (index word bw, data cur)
+          auto round = [&](int r0, uint32_t bw, const V &cur) {
+              const bool valid = r0 + lane < total;
+              const int be = bw_env(bw), bk = bw_slot(bw);
+              const bool bt0 = bw_t0(bw);
+              float bx[2 * NBOD2], by[2 * NBOD2];
 #pragma unroll
-            for (int u = 0; u < NBOD2; ++u) {
-                const float4 v = s_body[be][u];
-                bx[2 * u] = v.x;
-                by[2 * u] = v.y;
-                bx[2 * u + 1] = v.z;
-                by[2 * u + 1] = v.w;
-            }
-            const float xf = valid ? float(cur.x) : FAR_POS, yf = valid ? float(cur.y) : FAR_POS;
-            // float32 prefilter.  Planets only matter through the nearest one:
-            // below the band it is a certain hit, inside the band the exact
-            // tests run, above it no planet is hit.  Ships one by one (rewards)
-            float pmin = __builtin_huge_valf();
+              for (int u = 0; u < NBOD2; ++u) {
+                  const float4 v = s_body[be][u];
+                  bx[2 * u] = v.x;
+                  by[2 * u] = v.y;
+                  bx[2 * u + 1] = v.z;
+                  by[2 * u + 1] = v.w;
+              }
+              const float xf = valid ? float(cur.x) : FAR_POS, yf = valid ? float(cur.y) : FAR_POS;
+              // float32 prefilter.  Planets only matter through the nearest one:
+              // below the band it is a certain hit, inside the band the exact
+              // tests run, above it no planet is hit.  Ships one by one (rewards)
+              float pmin = __builtin_huge_valf();
 #pragma unroll
-            for (int j = 0; j < PMAX; ++j) {
-                const float dx = xf - bx[S + j], dy = yf - by[S + j];
-                pmin = __builtin_fminf(pmin, dx * dx + dy * dy);
-            }
-            bool bh = pmin < gp.lo;
-            bool amb = (pmin >= gp.lo) & (pmin <= gp.hi);
-            bool hs[S];
+              for (int j = 0; j < PMAX; ++j) {
+                  const float dx = xf - bx[S + j], dy = yf - by[S + j];
+                  pmin = __builtin_fminf(pmin, dx * dx + dy * dy);
+              }
+              bool bh = pmin < gp.lo;
+              bool amb = (pmin >= gp.lo) & (pmin <= gp.hi);
+              bool hs[S];
 #pragma unroll
-            for (int s = 0; s < S; ++s) hs[s] = near32(xf, yf, bx[s], by[s], gs, amb);
-            amb |= valid & bt0;
-            if (__any(amb)) {
-                if (amb) {   // exact tests; the old bodies are still in memory
-                    const size_t ie = size_t(base + be);
-                    const int bnp = bw_np(bw);
-                    const double x = double(cur.x), y = double(cur.y);
-                    bool bh64 = false;
+              for (int s = 0; s < S; ++s) hs[s] = near32(xf, yf, bx[s], by[s], gs, amb);
+              amb |= valid & bt0;
+              if (__any(amb)) {
+                  if (amb) {   // exact tests; the old bodies are still in memory
+                      const size_t ie = size_t(base + be);
+                      const int bnp = bw_np(bw);
+                      const double x = double(cur.x), y = double(cur.y);
+                      bool bh64 = false;
 #pragma unroll
-                    for (int j = 0; j < PMAX; ++j) {
-                        if (j < bnp) {
-                            const V pj = planets[size_t(j) * NN + ie];
-                            bh64 |= closer_exact(x, y, double(pj.x), double(pj.y), gp, bt0);
-                        }
-                    }
+                      for (int j = 0; j < PMAX; ++j) {
+                          if (j < bnp) {
+                              const V pj = planets[size_t(j) * NN + ie];
+                              bh64 |= closer_exact(x, y, double(pj.x), double(pj.y), gp, bt0);
+                          }
+                      }
 #pragma unroll
-                    for (int s = 0; s < S; ++s) {
-                        const V sj = ships[size_t(s) * NN + ie];
-                        hs[s] = closer_exact(x, y, double(sj.x), double(sj.y), gs, bt0);
-                    }
-                    bh = bh64;
-                }
-            }
-            bool ship_hit = false;
+                      for (int s = 0; s < S; ++s) {
+                          const V sj = ships[size_t(s) * NN + ie];
+                          hs[s] = closer_exact(x, y, double(sj.x), double(sj.y), gs, bt0);
+                      }
+                      bh = bh64;
+                  }
+              }
+              bool ship_hit = false;
 #pragma unroll
-            for (int s = 0; s < S; ++s) ship_hit |= hs[s];
-            bh |= ship_hit;
-            if (__any(ship_hit)) {   // rare: record which ships of the env were hit
-                const int hb = (hs[0] ? 1 : 0) | (S == 2 && hs[S - 1] ? 2 : 0);
-                if (hb) atomicOr(&s_hit[be], hb);   // (an invalid lane never hits: it sits at FAR_POS)
-            }
-            bool keep;
-            V out;
-            if (valid && bt0) {   // tick-0 bullets exist only in hand-made states
-                const float dtf = float(p.dt);
-                const float ndx = float(cur.z) + 0.0f, ndy = float(cur.w) + 0.0f;
-                const float nx = float(cur.x) + dtf * ndx, ny = float(cur.y) + dtf * ndy;
-                keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
-                out.x = T(nx);
-                out.y = T(ny);
-                out.z = T(ndx);
-                out.w = T(ndy);
-            } else {
-                // dx + 0 * dt in the state's own type: exact either way
-                const T ndx = cur.z + T(0), ndy = cur.w + T(0);
-                const double nx = double(cur.x) + dt * double(ndx), ny = double(cur.y) + dt * double(ndy);
-                keep = (__builtin_fabs(nx) <= 1.0) || (__builtin_fabs(ny) <= 1.0);   // -1 <= v <= 1
-                out.x = T(nx);
-                out.y = T(ny);
-                out.z = ndx;
-                out.w = ndy;
-            }
-            keep = keep & valid & !bh;
-            const uint64_t kb = __ballot(keep);
-            const int kg = kept_before + __popcll(kb & lanes_below);
-            const int first = lane - bk;   // lane of the env's slot 0 (< 0: an earlier round)
-            const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
-            const int pos = kg - k0;
-            if (keep) bullets[size_t(base + be) * BC + pos] = out;
-            if (valid && bw_last(bw)) s_kept[be] = pos + int(keep);
-            carry = __builtin_amdgcn_readlane(k0, 63);
-            kept_before += __popcll(kb);
+              for (int s = 0; s < S; ++s) ship_hit |= hs[s];
+              bh |= ship_hit;
+              if (__any(ship_hit)) {   // rare: record which ships of the env were hit
+                  const int hb = (hs[0] ? 1 : 0) | (S == 2 && hs[S - 1] ? 2 : 0);
+                  if (hb) atomicOr(&s_hit[be], hb);   // (an invalid lane never hits: it sits at FAR_POS)
+              }
+              bool keep;
+              V out;
+              if (valid && bt0) {   // tick-0 bullets exist only in hand-made states
+                  const float dtf = float(p.dt);
+                  const float ndx = float(cur.z) + 0.0f, ndy = float(cur.w) + 0.0f;
+                  const float nx = float(cur.x) + dtf * ndx, ny = float(cur.y) + dtf * ndy;
+                  keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
+                  out.x = T(nx);
+                  out.y = T(ny);
+                  out.z = T(ndx);
+                  out.w = T(ndy);
+              } else {
+                  // dx + 0 * dt in the state's own type: exact either way
+                  const T ndx = cur.z + T(0), ndy = cur.w + T(0);
+                  const double nx = double(cur.x) + dt * double(ndx), ny = double(cur.y) + dt * double(ndy);
+                  keep = (__builtin_fabs(nx) <= 1.0) || (__builtin_fabs(ny) <= 1.0);   // -1 <= v <= 1
+                  out.x = T(nx);
+                  out.y = T(ny);
+                  out.z = ndx;
+                  out.w = ndy;
+              }
+              keep = keep & valid & !bh;
+              const uint64_t kb = __ballot(keep);
+              const int kg = kept_before + __popcll(kb & lanes_below);
+              const int first = lane - bk;   // lane of the env's slot 0 (< 0: an earlier round)
+              const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
+              const int pos = kg - k0;
+              if (keep) bullets[size_t(base + be) * BC + pos] = out;
+              if (valid && bw_last(bw)) s_kept[be] = pos + int(keep);
+              carry = __builtin_amdgcn_readlane(k0, 63);
+              kept_before += __popcll(kb);
+          };
+          // The first rounds straight-line (a wave of 32 envs carries ~164
+          // bullets): each round's data was loaded a round or more ahead and
+          // no register rotation sits between a load and its use, so the
+          // waits before a round cover its own load only, never the previous
+          // round's stores (a loop with rotating prefetch registers waited
+          // vmcnt(0) -- every store -- at each round)
+          uint32_t bw2 = 0u;
+          V cur2 = cur0;
+          if (w0 + 128 < wend) {
+              bw2 = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
+              cur2 = bullets[size_t(base + bw_env(bw2)) * BC + bw_slot(bw2)];
+          }
+          round(w0, bw0, cur0);
+          if (w0 + 64 < wend) round(w0 + 64, bw1, cur1);
+          if (w0 + 128 < wend) round(w0 + 128, bw2, cur2);
+          for (int r0 = w0 + 192; r0 < wend; r0 += 64) {   // uniform; rare
+              const uint32_t bw = r0 + lane < wend ? s_index[r0 + lane - w0] : 0u;
+              const V cur = bullets[size_t(base + bw_env(bw)) * BC + bw_slot(bw)];
+              round(r0, bw, cur);
           }
         }
     }
