@@ -1594,115 +1594,164 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
               cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
           }
           // one round: lane g takes live bullet r0 + g (index word bw, data cur)
-          auto round = [&](int r0, uint32_t bw, const V &cur) {
-              const bool valid = r0 + lane < total;
-              const int be = bw_env(bw), bk = bw_slot(bw);
-              const bool bt0 = bw_t0(bw);
-              float bx[2 * NBOD2], by[2 * NBOD2];
+          // NR rounds at once, lane g of round r taking live bullet r0 + 64 r + g
+          // (index words bws[r], data curs[r]): their collision tests and moves
+          // are independent, so they are evaluated side by side (the latency
+          // chains of one round overlap the other's: a pair-kernel SIMD has
+          // only two waves to switch between); the compaction then runs round
+          // by round, in order
+          auto rounds = [&](auto nr_tag, int r0, const uint32_t *bws, const V *curs) {
+              constexpr int NR = decltype(nr_tag)::value;
+              bool valid[NR], amb[NR], bh[NR], bt0[NR], hs[NR][S];
+              int be[NR];
 #pragma unroll
-              for (int u = 0; u < NBOD2; ++u) {
-                  const float4 v = s_body[be][u];
-                  bx[2 * u] = v.x;
-                  by[2 * u] = v.y;
-                  bx[2 * u + 1] = v.z;
-                  by[2 * u + 1] = v.w;
+              for (int r = 0; r < NR; ++r) {
+                  valid[r] = r0 + 64 * r + lane < total;
+                  be[r] = bw_env(bws[r]);
+                  bt0[r] = bw_t0(bws[r]);
+                  float bx[2 * NBOD2], by[2 * NBOD2];
+#pragma unroll
+                  for (int u = 0; u < NBOD2; ++u) {
+                      const float4 v = s_body[be[r]][u];
+                      bx[2 * u] = v.x;
+                      by[2 * u] = v.y;
+                      bx[2 * u + 1] = v.z;
+                      by[2 * u + 1] = v.w;
+                  }
+                  const float xf = valid[r] ? float(curs[r].x) : FAR_POS;
+                  const float yf = valid[r] ? float(curs[r].y) : FAR_POS;
+                  // float32 prefilter.  Planets only matter through the nearest
+                  // one: below the band it is a certain hit, inside the band the
+                  // exact tests run, above it no planet is hit.  Ships one by one
+                  float pmin = __builtin_huge_valf();
+#pragma unroll
+                  for (int j = 0; j < PMAX; ++j) {
+                      const float dx = xf - bx[S + j], dy = yf - by[S + j];
+                      pmin = __builtin_fminf(pmin, dx * dx + dy * dy);
+                  }
+                  bh[r] = pmin < gp.lo;
+                  bool am = (pmin >= gp.lo) & (pmin <= gp.hi);
+#pragma unroll
+                  for (int s = 0; s < S; ++s) hs[r][s] = near32(xf, yf, bx[s], by[s], gs, am);
+                  amb[r] = am | (valid[r] & bt0[r]);
               }
-              const float xf = valid ? float(cur.x) : FAR_POS, yf = valid ? float(cur.y) : FAR_POS;
-              // float32 prefilter.  Planets only matter through the nearest one:
-              // below the band it is a certain hit, inside the band the exact
-              // tests run, above it no planet is hit.  Ships one by one (rewards)
-              float pmin = __builtin_huge_valf();
+              bool any_amb = false;
 #pragma unroll
-              for (int j = 0; j < PMAX; ++j) {
-                  const float dx = xf - bx[S + j], dy = yf - by[S + j];
-                  pmin = __builtin_fminf(pmin, dx * dx + dy * dy);
-              }
-              bool bh = pmin < gp.lo;
-              bool amb = (pmin >= gp.lo) & (pmin <= gp.hi);
-              bool hs[S];
+              for (int r = 0; r < NR; ++r) any_amb |= amb[r];
+              if (__any(any_amb)) {   // rare: the exact tests; the old bodies are still in memory
 #pragma unroll
-              for (int s = 0; s < S; ++s) hs[s] = near32(xf, yf, bx[s], by[s], gs, amb);
-              amb |= valid & bt0;
-              if (__any(amb)) {
-                  if (amb) {   // exact tests; the old bodies are still in memory
-                      const size_t ie = size_t(base + be);
-                      const int bnp = bw_np(bw);
-                      const double x = double(cur.x), y = double(cur.y);
-                      bool bh64 = false;
+                  for (int r = 0; r < NR; ++r) {
+                      if (amb[r]) {
+                          const size_t ie = size_t(base + be[r]);
+                          const int bnp = bw_np(bws[r]);
+                          const double x = double(curs[r].x), y = double(curs[r].y);
+                          bool bh64 = false;
 #pragma unroll
-                      for (int j = 0; j < PMAX; ++j) {
-                          if (j < bnp) {
-                              const V pj = planets[size_t(j) * NN + ie];
-                              bh64 |= closer_exact(x, y, double(pj.x), double(pj.y), gp, bt0);
+                          for (int j = 0; j < PMAX; ++j) {
+                              if (j < bnp) {
+                                  const V pj = planets[size_t(j) * NN + ie];
+                                  bh64 |= closer_exact(x, y, double(pj.x), double(pj.y), gp, bt0[r]);
+                              }
                           }
-                      }
 #pragma unroll
-                      for (int s = 0; s < S; ++s) {
-                          const V sj = ships[size_t(s) * NN + ie];
-                          hs[s] = closer_exact(x, y, double(sj.x), double(sj.y), gs, bt0);
+                          for (int s = 0; s < S; ++s) {
+                              const V sj = ships[size_t(s) * NN + ie];
+                              hs[r][s] = closer_exact(x, y, double(sj.x), double(sj.y), gs, bt0[r]);
+                          }
+                          bh[r] = bh64;
                       }
-                      bh = bh64;
                   }
               }
-              bool ship_hit = false;
+              bool any_hit = false;
 #pragma unroll
-              for (int s = 0; s < S; ++s) ship_hit |= hs[s];
-              bh |= ship_hit;
-              if (__any(ship_hit)) {   // rare: record which ships of the env were hit
-                  const int hb = (hs[0] ? 1 : 0) | (S == 2 && hs[S - 1] ? 2 : 0);
-                  if (hb) atomicOr(&s_hit[be], hb);   // (an invalid lane never hits: it sits at FAR_POS)
+              for (int r = 0; r < NR; ++r) {
+                  bool ship_hit = false;
+#pragma unroll
+                  for (int s = 0; s < S; ++s) ship_hit |= hs[r][s];
+                  bh[r] |= ship_hit;
+                  any_hit |= ship_hit;
               }
-              bool keep;
-              V out;
-              if (valid && bt0) {   // tick-0 bullets exist only in hand-made states
-                  const float dtf = float(p.dt);
-                  const float ndx = float(cur.z) + 0.0f, ndy = float(cur.w) + 0.0f;
-                  const float nx = float(cur.x) + dtf * ndx, ny = float(cur.y) + dtf * ndy;
-                  keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
-                  out.x = T(nx);
-                  out.y = T(ny);
-                  out.z = T(ndx);
-                  out.w = T(ndy);
-              } else {
+              if (__any(any_hit)) {   // rare: record which ships of the env were hit
+#pragma unroll
+                  for (int r = 0; r < NR; ++r) {
+                      const int hb = (hs[r][0] ? 1 : 0) | (S == 2 && hs[r][S - 1] ? 2 : 0);
+                      if (hb) atomicOr(&s_hit[be[r]], hb);   // (an invalid lane never hits: it sits at FAR_POS)
+                  }
+              }
+              // move without gravity and cull (core.py:295-300, 195)
+              bool keep[NR];
+              V out[NR];
+              bool any_t0 = false;
+#pragma unroll
+              for (int r = 0; r < NR; ++r) {
                   // dx + 0 * dt in the state's own type: exact either way
+                  const V &cur = curs[r];
                   const T ndx = cur.z + T(0), ndy = cur.w + T(0);
                   const double nx = double(cur.x) + dt * double(ndx), ny = double(cur.y) + dt * double(ndy);
-                  keep = (__builtin_fabs(nx) <= 1.0) || (__builtin_fabs(ny) <= 1.0);   // -1 <= v <= 1
-                  out.x = T(nx);
-                  out.y = T(ny);
-                  out.z = ndx;
-                  out.w = ndy;
+                  keep[r] = (__builtin_fabs(nx) <= 1.0) || (__builtin_fabs(ny) <= 1.0);   // -1 <= v <= 1
+                  out[r].x = T(nx);
+                  out[r].y = T(ny);
+                  out[r].z = ndx;
+                  out[r].w = ndy;
+                  any_t0 |= valid[r] & bt0[r];
               }
-              keep = keep & valid & !bh;
-              const uint64_t kb = __ballot(keep);
-              const int kg = kept_before + __popcll(kb & lanes_below);
-              const int first = lane - bk;   // lane of the env's slot 0 (< 0: an earlier round)
-              const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
-              const int pos = kg - k0;
-              if (keep) bullets[size_t(base + be) * BC + pos] = out;
-              if (valid && bw_last(bw)) s_kept[be] = pos + int(keep);
-              carry = __builtin_amdgcn_readlane(k0, 63);
-              kept_before += __popcll(kb);
+              if (__any(any_t0)) {   // tick-0 bullets exist only in hand-made states: float32
+                  const float dtf = float(p.dt);
+#pragma unroll
+                  for (int r = 0; r < NR; ++r) {
+                      if (valid[r] && bt0[r]) {
+                          const V &cur = curs[r];
+                          const float ndx = float(cur.z) + 0.0f, ndy = float(cur.w) + 0.0f;
+                          const float nx = float(cur.x) + dtf * ndx, ny = float(cur.y) + dtf * ndy;
+                          keep[r] = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
+                          out[r].x = T(nx);
+                          out[r].y = T(ny);
+                          out[r].z = T(ndx);
+                          out[r].w = T(ndy);
+                      }
+                  }
+              }
+              // compaction in slot order, round by round
+#pragma unroll
+              for (int r = 0; r < NR; ++r) {
+                  const bool kp = keep[r] & valid[r] & !bh[r];
+                  const uint64_t kb = __ballot(kp);
+                  const int kg = kept_before + __popcll(kb & lanes_below);
+                  const int first = lane - bw_slot(bws[r]);   // lane of the env's slot 0 (< 0: an earlier round)
+                  const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
+                  const int pos = kg - k0;
+                  if (kp) bullets[size_t(base + be[r]) * BC + pos] = out[r];
+                  if (valid[r] && bw_last(bws[r])) s_kept[be[r]] = pos + int(kp);
+                  carry = __builtin_amdgcn_readlane(k0, 63);
+                  kept_before += __popcll(kb);
+              }
           };
-          // The first rounds straight-line (a wave of 32 envs carries ~164
-          // bullets): each round's data was loaded a round or more ahead and
-          // no register rotation sits between a load and its use, so the
-          // waits before a round cover its own load only, never the previous
-          // round's stores (a loop with rotating prefetch registers waited
-          // vmcnt(0) -- every store -- at each round)
-          uint32_t bw2 = 0u;
-          V cur2 = cur0;
-          if (w0 + 128 < wend) {
-              bw2 = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
-              cur2 = bullets[size_t(base + bw_env(bw2)) * BC + bw_slot(bw2)];
+          // The first rounds straight-line: each round's data was loaded a
+          // round or more ahead and no register rotation sits between a load
+          // and its use, so the waits before a round cover its own load only,
+          // never an earlier round's stores (a loop with rotating prefetch
+          // registers waited vmcnt(0) -- every store -- at each round)
+          uint32_t bws[3] = {bw0, bw1, 0u};
+          V curs[3] = {cur0, cur1, cur0};
+          const int nr = (wend - w0 + 63) / 64;   // uniform
+          // two rounds side by side with 4 planet slots; with 8 the registers
+          // of two rounds spill (measured: c5 30.8 -> 34.3 us), one at a time
+          constexpr int NR2 = PMAX <= 4 ? 2 : 1;
+          if (nr >= 3) {
+              bws[2] = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
+              curs[2] = bullets[size_t(base + bw_env(bws[2])) * BC + bw_slot(bws[2])];
           }
-          round(w0, bw0, cur0);
-          if (w0 + 64 < wend) round(w0 + 64, bw1, cur1);
-          if (w0 + 128 < wend) round(w0 + 128, bw2, cur2);
+          if (nr >= 2) {
+              rounds(std::integral_constant<int, NR2>(), w0, bws, curs);
+              if (NR2 == 1) rounds(std::integral_constant<int, 1>(), w0 + 64, bws + 1, curs + 1);
+          } else {
+              rounds(std::integral_constant<int, 1>(), w0, bws, curs);
+          }
+          if (nr >= 3) rounds(std::integral_constant<int, 1>(), w0 + 128, bws + 2, curs + 2);
           for (int r0 = w0 + 192; r0 < wend; r0 += 64) {   // uniform; rare
               const uint32_t bw = r0 + lane < wend ? s_index[r0 + lane - w0] : 0u;
               const V cur = bullets[size_t(base + bw_env(bw)) * BC + bw_slot(bw)];
-              round(r0, bw, cur);
+              rounds(std::integral_constant<int, 1>(), r0, &bw, &cur);
           }
         }
     }
@@ -1934,7 +1983,7 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 
 template <typename T, int S, int PMAX, bool MULTI, int LPE>
-__global__ __launch_bounds__(QBLOCK, 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+__global__ __launch_bounds__(QBLOCK, MULTI ? 2 : 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {

@@ -60,7 +60,7 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
     use_lib(lib)
     env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, kernel=kernel)
     env.reset()
-    nw = (n + 63) // 64 if kernel == 'lane' else (n + 15) // 16
+    nw = (n + 63) // 64 if kernel == 'lane' else ((n + 31) // 32 if kernel == 'pair' else (n + 15) // 16)
     ncr = 0
     env.stats = torch.zeros(nw + ncr, 16, dtype=torch.int64, device='cuda')
     ctl = torch.from_numpy(bench.controls(0, n, env.S, warm + ticks)).cuda()
@@ -215,6 +215,10 @@ def main():
             run(lib + ':c2', D._replace(reload_time=1000), 65536)
             run(lib + ':c3_noreset', D, 65536, auto_reset=False)
             stamps(lib + ':c3', D, 65536, lib=lib + '_stamps.so')
+        return
+    if a.set == 'stamps_pair':
+        stamps('pair_c3', D, 65536, kernel='pair')
+        stamps('quad_c3', D, 65536, kernel='quad')
         return
     if a.set == 'stamps':
         stamps('quad_c3', D, 65536, kernel='quad')
