@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'reserved')
@@ -43,7 +43,7 @@ class AstroParams(ctypes.Structure):
         ('timeout_tick', ctypes.c_int32),
         ('fire_bits', ctypes.c_void_p),
         ('kernel', ctypes.c_int32),
-        ('reserved', ctypes.c_int32),
+        ('planets_only', ctypes.c_int32),
         ('key_table', ctypes.c_void_p),
     ]
 

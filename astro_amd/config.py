@@ -44,5 +44,19 @@ def generate_configs(config):
         yield config._replace(seed=random.randint(1 << 30))
 
 
+def create_nplanets(config, seed):
+    """The number of planets create() draws for ``seed`` (core.py:90)."""
+    return int(np.random.RandomState(seed).randint(1, config.max_planets + 1))
+
+
+def generate_configs_filtered(config, planets):
+    """generate_configs(config) restricted to the seeds whose game has exactly
+    ``planets`` planets -- the game sequence of BatchedEnv(planets_only=...),
+    used for BASELINE.json's fixed-planet-count workloads."""
+    for cfg in generate_configs(config):
+        if create_nplanets(cfg, cfg.seed) == planets:
+            yield cfg
+
+
 def nships(config):
     return 1 if config.solo else 2

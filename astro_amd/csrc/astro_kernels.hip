@@ -348,6 +348,20 @@ __device__ __forceinline__ uint32_t key397_of(const AstroParams &p, uint32_t see
     return mt_key_at(seed, 0, MT_PROLOGUE);
 }
 
+// planets_only (AstroParams): the number of planets create() draws for
+// `seed` -- randint(1, max_planets + 1) on RandomState(seed)'s first word,
+// which alone decides it when max_planets is a power of two (checked on the
+// host) -- and whether the seed's game passes the filter.
+__device__ __forceinline__ int first_nplanets(const AstroParams &p, uint32_t seed, uint32_t key397) {
+    const uint32_t a1 = mt_key_next(seed, 1u);
+    const uint32_t y = (seed & 0x80000000u) | (a1 & 0x7fffffffu);
+    const uint32_t w = mt_temper(key397 ^ (y >> 1) ^ ((a1 & 1u) ? 0x9908b0dfu : 0u));
+    return 1 + int(w & uint32_t(p.max_planets - 1));
+}
+__device__ __forceinline__ bool seed_passes(const AstroParams &p, uint32_t seed, uint32_t key397) {
+    return p.planets_only == 0 || first_nplanets(p, seed, key397) == p.planets_only;
+}
+
 constexpr double TWO_PI = 6.283185307179586;  // 2 * np.pi
 constexpr double PI = 3.141592653589793;      // np.pi
 
@@ -550,6 +564,8 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, con
 // pending seed and the stream cursor advanced by one game (core.py:83).
 template <int S>
 struct NextGame {
+    uint32_t seed;         // the game's seed (the pending seed, or with
+                           // planets_only the first of the stream to pass)
     CreateWords<S> words;
     uint32_t ca, cb, ci;   // advanced cursor
     uint32_t next_seed;    // the game after
@@ -561,11 +577,20 @@ template <int S>
 __device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t pend_seed, uint32_t key397,
                                                  bool have_key, uint32_t ca, uint32_t cb, uint32_t ci) {
     NextGame<S> ng;
-    ng.words = create_words<S>(p, pend_seed, have_key ? key397 : mt_key_at(pend_seed, 0, MT_PROLOGUE));
     MTLazy g;
     g.a = ca;
     g.b = cb;
     g.i = ci;
+    if (!have_key) key397 = mt_key_at(pend_seed, 0, MT_PROLOGUE);
+    // planets_only: the pending seed may not have been checked yet (a game
+    // shorter than the steps that check one candidate each): walk the
+    // stream here, synchronously
+    while (!seed_passes(p, pend_seed, key397) && g.ok()) {
+        pend_seed = g.next() & SEED_MASK;
+        key397 = key397_of(p, pend_seed);
+    }
+    ng.seed = pend_seed;
+    ng.words = create_words<S>(p, pend_seed, key397);
     ng.exhausted = !g.ok() || ng.words.exhausted;
     ng.next_seed = g.next() & SEED_MASK;
     ng.ca = g.a;
@@ -577,14 +602,37 @@ __device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t 
 // Start env i's next game from its NextGame: create (the float half), then
 // the stream record and header (part 0).
 template <typename T, int S, int PMAX, int NPART = 1>
-__device__ __forceinline__ void restart_env(const AstroParams &p, const AstroState &st, int i, uint32_t pend_seed,
+__device__ __forceinline__ void restart_env(const AstroParams &p, const AstroState &st, int i,
                                             const NextGame<S> &ng, int part = 0) {
     int cf = 0;
     const int n = create_env<T, S, PMAX, NPART>(p, st, i, create_draws<S>(ng.words), cf, part);
     if (part != 0) return;
-    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(ng.ca, ng.cb, ng.ci, pend_seed);
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(ng.ca, ng.cb, ng.ci, ng.seed);
     const int flags = (ng.exhausted || cf) ? 2 : 0;
     reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(ng.next_seed), 0);
+}
+
+// The pending seed at the end of a step (the lane holding the env's header):
+// key[397] of a pending seed is gathered by the first step that finds it
+// missing (KEY_VALID); with planets_only, that step also checks the seed and,
+// if its game has the wrong number of planets, draws the stream's next one
+// instead (cursor c, loaded beside the gather) for the following step to
+// check -- one candidate per step, off the reset path.  Returns the
+// KEY_VALID bit for the header.
+__device__ __forceinline__ uint32_t check_pending(const AstroParams &p, const AstroState &st, int i, bool key_valid,
+                                                  const uint4 &c, uint32_t &seed, uint32_t &key) {
+    if (key_valid) return KEY_VALID;
+    if (!p.key_table) return 0u;
+    if (seed_passes(p, seed, key)) return KEY_VALID;
+    MTLazy g;
+    g.a = c.x;
+    g.b = c.y;
+    g.i = c.z;
+    if (!g.ok()) return KEY_VALID;   // stream exhausted (flagged at the game's create): keep it
+    seed = g.next() & SEED_MASK;
+    key = 0u;
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, c.w);
+    return 0u;
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -820,7 +868,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         }
         const int tick = int(uint32_t(h.x) & TICK_MASK);
         const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
-        const uint32_t pend_seed = uint32_t(h.z);
+        uint32_t pend_seed = uint32_t(h.z);
         int np = h.y & 0xff;
         int flags = (h.y >> 8) & 0xff;
         const int nb = int(uint32_t(h.y) >> 16);
@@ -846,6 +894,8 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         // key[397] of the next game's seed, fetched once per game, off the reset path
         uint32_t pend_key = uint32_t(h.w);
         if (!key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
+        uint4 c_pend = make_uint4(0u, 0u, 0u, 0u);   // stream cursor, for check_pending
+        if (!key_valid && p.key_table && p.planets_only) c_pend = reinterpret_cast<const uint4 *>(st.stream)[i];
         V buf[BCHUNK];
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) {
@@ -1016,7 +1066,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             }
             STAMP(7);
             if (dropped) flags |= 1;
-            const uint32_t kv = (key_valid || p.key_table) ? KEY_VALID : 0u;
+            const uint32_t kv = check_pending(p, st, i, key_valid, c_pend, pend_seed, pend_key);
             reinterpret_cast<int4 *>(st.hdr)[i] =
                 make_int4(int(uint32_t(tick + 1) | kv), np | (flags << 8) | (w << 16), int(pend_seed), int(pend_key));
             n_bout = uint32_t(w);
@@ -1029,7 +1079,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             if (auto_reset) {
                 const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
                 const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, c.x, c.y, c.z);
-                restart_env<T, S, PMAX>(p, st, i, pend_seed, ng);
+                restart_env<T, S, PMAX>(p, st, i, ng);
                 f_reset = true;
             }
             STAMP(10);
@@ -1319,7 +1369,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     mask |= mask >> 8;
     mask |= mask >> 16;
     const uint32_t v = uint32_t(__shfl(int(w), row0, 64)) & mask;
-    const bool fast = rng != 0 && v <= rng;
+    const bool fast = rng != 0 && v <= rng && (p.planets_only == 0 || int(v) + 1 == p.planets_only);
     // lane k of the row: R_k = rand() of outputs k, k + 1
     const uint32_t wn = uint32_t(__shfl(int(w), row0 | ((u + 1) & 15), 64));
     const double R = rand53(w, wn);
@@ -1437,7 +1487,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     }
     const int tick = int(uint32_t(h.x) & TICK_MASK);
     const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
-    const uint32_t pend_seed = uint32_t(h.z);
+    uint32_t pend_seed = uint32_t(h.z);
     int np = h.y & 0xff;
     const int flags = (h.y >> 8) & 0xff;
     const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
@@ -1476,6 +1526,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // gather into the 4 GiB key table, issued after every load the physics
     // waits for, so only its consumers (header store, reset) wait for it
     if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
+    uint4 c_pend = make_uint4(0u, 0u, 0u, 0u);   // stream cursor, for check_pending
+    if (q == 0 && !key_valid && p.key_table && p.planets_only) c_pend = reinterpret_cast<const uint4 *>(st.stream)[i];
 
     // ---- quad broadcasts: all planets, both ships
     double px[PMAX], py[PMAX], sx[S], sy[S];
@@ -1893,7 +1945,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             STAMP(7);
             if (q == 0) {
                 const int fl = flags | (dropped ? 1 : 0);
-                const uint32_t kv = (key_valid || p.key_table) ? KEY_VALID : 0u;
+                const uint32_t kv = check_pending(p, st, is, key_valid, c_pend, pend_seed, pend_key);
                 reinterpret_cast<int4 *>(st.hdr)[is] =
                     make_int4(int(uint32_t(tick + 1) | kv), np | (fl << 8) | (w << 16), int(pend_seed), int(pend_key));
                 n_bout += uint32_t(w);
@@ -1921,7 +1973,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(pend_key)));   // lane q == 0 fetched it
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
             const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, c.x, c.y, c.z);
-            restart_env<T, S, PMAX, LPE>(p, st, is, pend_seed, ng, q);
+            restart_env<T, S, PMAX, LPE>(p, st, is, ng, q);
         }
     }
     STAMP(10);
@@ -2099,7 +2151,7 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
         const uint32_t seed = uint32_t(h.z);
         const uint32_t key = (uint32_t(h.x) & KEY_VALID) ? uint32_t(h.w) : key397_of(p, seed);
         const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-        restart_env<T, S, PMAX>(p, st, i, seed, next_game<S>(p, seed, key, true, c.x, c.y, c.z));
+        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, c.x, c.y, c.z));
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued
@@ -2183,6 +2235,10 @@ int check_params(const AstroParams *p) {
     if (p->timeout_tick < 0 || p->timeout_tick >= int(TICK_MASK)) return fail(-16, "timeout_tick out of [0, 2^22)");
     if (p->timeout_tick > 0 && !p->fire_bits) return fail(-17, "fire_bits is NULL");
     if (p->kernel < 0 || p->kernel > 3) return fail(-18, "kernel must be 0 (auto), 1 (lane), 2 (quad) or 3 (pair)");
+    if (p->planets_only < 0 || p->planets_only > p->max_planets)
+        return fail(-19, "planets_only must be in [0, max_planets]");
+    if (p->planets_only && (p->max_planets & (p->max_planets - 1)))
+        return fail(-19, "planets_only needs max_planets a power of two (one MT word decides the count)");
     return 0;
 }
 

@@ -81,12 +81,21 @@ class BatchedEnv:
                   per env) or 'pair' (two); identical results, different speed
     use_key_table -- share the device's 4 GiB seeding table (see key_table);
                   False runs every game's 397-step chain inline (same results)
+    planets_only -- 0, or P: each env's games are its generate_configs stream
+                  filtered to the seeds whose create() draws exactly P planets
+                  (config.generate_configs_filtered); max_planets must be a
+                  power of two
     """
 
     def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
                  dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto',
-                 use_key_table=True):
+                 use_key_table=True, planets_only=0):
         _schedule.check_config(config)
+        planets_only = int(planets_only)
+        if planets_only and (not 1 <= planets_only <= config.max_planets
+                             or config.max_planets & (config.max_planets - 1)):
+            raise ValueError('planets_only must be in [1, max_planets], max_planets a power of two')
+        self.planets_only = planets_only
         if dtype not in (torch.float32, torch.float64):
             raise ValueError('dtype must be torch.float32 or torch.float64')
         self.lib = _lib.load()
@@ -122,7 +131,7 @@ class BatchedEnv:
         self.key_table = key_table(dev) if use_key_table else None
         self.params = _lib.AstroParams(
             p_pad=self.p_pad, b_cap=self.b_cap, timeout_tick=self.schedule.timeout_tick,
-            fire_bits=self.fire_bits.data_ptr(), kernel=_lib.KERNELS[kernel],
+            fire_bits=self.fire_bits.data_ptr(), kernel=_lib.KERNELS[kernel], planets_only=planets_only,
             key_table=self.key_table.data_ptr() if self.key_table is not None else None, **k)
         self.state = _lib.AstroState(
             ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),

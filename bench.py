@@ -31,13 +31,18 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # BASELINE.json configs 2, 3 and 5 (per GPU); configs 4 = c3 on 8 GPUs
 WORKLOADS = {
-    'c2': dict(n=4096, cfg=dict(reload_time=1000), b_cap=32, p_pad=4,
+    'c2': dict(n=4096, cfg=dict(reload_time=1000), b_cap=32, p_pad=4, planets_only=3,
                desc='4096 envs/GPU, DEFAULT_CONFIG with bullets disabled (reload_time=1000), '
-                    '2 ships, 1-4 planets, auto-reset, random actions'),
-    'c3': dict(n=65536, cfg=dict(), b_cap=32, p_pad=4,
-               desc='65536 envs/GPU, DEFAULT_CONFIG (2 ships, 1-4 planets, bullets on, '
-                    'b_cap 32 = 16/ship + overflow counter), auto-reset, random actions'),
-    'c5': dict(n=131072, cfg=dict(max_planets=8), b_cap=32, p_pad=8,
+                    '2 ships, 3 planets (generate_configs streams filtered to 3-planet games), '
+                    'auto-reset, random actions'),
+    'c3': dict(n=65536, cfg=dict(), b_cap=32, p_pad=4, planets_only=3,
+               desc='65536 envs/GPU, DEFAULT_CONFIG (2 ships, 3 planets: generate_configs streams '
+                    'filtered to 3-planet games; bullets on, b_cap 32 = 16/ship + overflow counter), '
+                    'auto-reset, random actions'),
+    'c3any': dict(n=65536, cfg=dict(), b_cap=32, p_pad=4, planets_only=0,
+                  desc='65536 envs/GPU, DEFAULT_CONFIG unfiltered (2 ships, 1-4 planets), bullets on, '
+                       'auto-reset, random actions'),
+    'c5': dict(n=131072, cfg=dict(max_planets=8), b_cap=32, p_pad=8, planets_only=0,
                desc='131072 envs/GPU, DEFAULT_CONFIG with max_planets=8 (1-8 planets padded '
                     'to 8), bullets on, auto-reset, random actions'),
 }
@@ -60,25 +65,26 @@ def controls(offset, n, nships, ticks, seed=0):
 
 
 def _cpu_worker(args):
-    cfg_kw, seconds, seed = args
+    cfg_kw, seconds, seed, planets_only = args
     from oracle import port
-    return port.run_for(DEFAULT_CONFIG._replace(**cfg_kw), seconds, seed=seed)
+    return port.run_for(DEFAULT_CONFIG._replace(**cfg_kw), seconds, seed=seed, planets_only=planets_only)
 
 
-def cpu_baseline(cfg_kw, seconds, procs):
+def cpu_baseline(cfg_kw, seconds, procs, planets_only=0):
     """The single-game numpy port of core.step (oracle/port.py, pinned bit
     for bit to the reference) on `procs` host cores, one game per process."""
     if procs == 1:
-        res = [_cpu_worker((cfg_kw, seconds, 0))]
+        res = [_cpu_worker((cfg_kw, seconds, 0, planets_only))]
     else:
         with mp.get_context('spawn').Pool(procs) as pool:
-            res = pool.map(_cpu_worker, [(cfg_kw, seconds, k) for k in range(procs)])
+            res = pool.map(_cpu_worker, [(cfg_kw, seconds, k, planets_only) for k in range(procs)])
     steps = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return dict(value=steps / wall, unit='env-steps/s', cores=procs, kind='port',
                 sample='%d x %.0f s of single-game oracle/port.py step() (numpy restatement of '
                        'core.step, bit-exact to the reference), random actions, re-create on '
-                       'termination: %d env-steps' % (procs, seconds, steps),
+                       'termination%s: %d env-steps' % (procs, seconds, ' (3-planet games)' if planets_only else '',
+                                                        steps),
                 per_core=steps / wall / procs)
 
 
@@ -142,7 +148,7 @@ def main():
     offset = rank * n
     env = BatchedEnv(cfg, n, device=dev, b_cap=wl['b_cap'], p_pad=wl['p_pad'],
                      dtype=torch.float64 if args.state == 'f64' else torch.float32,
-                     env_offset=offset, auto_reset=True, kernel=args.kernel)
+                     env_offset=offset, auto_reset=True, kernel=args.kernel, planets_only=wl['planets_only'])
     env.reset()
     ticks = args.warmup + args.steps
     ctl = torch.from_numpy(controls(offset, n, env.S, ticks)).to(dev)
@@ -295,7 +301,7 @@ def main():
         )
         out.update(extras)
         if world == 1 and not args.no_cpu:
-            out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, args.cpu_procs)
+            out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, args.cpu_procs, wl['planets_only'])
             out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 8
+#define ASTRO_ABI_VERSION 9
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -68,7 +68,10 @@ typedef struct AstroParams {
     int32_t timeout_tick;  /* first tick k with max_time <= t_k + dt */
     const uint32_t *fire_bits; /* device: bit k = fire on tick k, k < timeout_tick */
     int32_t kernel;        /* ASTRO_KERNEL_AUTO / _LANE / _QUAD / _PAIR (results are identical) */
-    int32_t reserved;
+    int32_t planets_only;  /* 0, or P: an env's games are its generate_configs stream
+                              (core.py:77-83) filtered to the seeds whose create()
+                              draws P planets; max_planets must be a power of two
+                              (one MT word decides), needs key_table for speed */
     const uint32_t *key_table; /* device, optional: key[397] of MT19937 init_genrand for
                                   every seed < 2^30 (astro_keytable_build); NULL = the
                                   397-step chain at each create (~9 us per lane) */

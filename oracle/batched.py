@@ -373,6 +373,23 @@ def game_seeds(env_stream_seeds, n_games):
     return (w & np.uint64((1 << 30) - 1)).astype(np.uint32)
 
 
+def filtered_game_seeds(env_stream_seeds, n_games, planets, max_planets, draws=200):
+    """[N, n_games] seeds of each env's successive games when its
+    generate_configs stream is filtered to games of exactly ``planets``
+    planets (BatchedEnv(planets_only=...)): create()'s randint(1,
+    max_planets + 1) (core.py:90) is the first word of RandomState(seed)
+    masked, max_planets a power of two."""
+    cand = game_seeds(env_stream_seeds, draws)                       # [N, draws]
+    first = mt19937.words(cand.reshape(-1), 1).reshape(cand.shape)
+    n = 1 + (first & np.uint32(max_planets - 1)).astype(np.int64)
+    out = np.zeros((len(env_stream_seeds), n_games), np.uint32)
+    for i in range(len(env_stream_seeds)):
+        ok = cand[i][n[i] == planets]
+        assert len(ok) >= n_games, 'increase draws'
+        out[i] = ok[:n_games]
+    return out
+
+
 def collisions_allpairs(x, r):
     """Generic all-pairs collision mask (core.py:200-212): body i is hit iff
     some other body j has |x_i - x_j|^2 < (r_i + r_j)^2 (strict, self

@@ -107,13 +107,23 @@ class Game:
         return nxt, np.zeros(ns, dtype=np.float32)
 
 
-def run_for(config, seconds, seed=0):
+def run_for(config, seconds, seed=0, planets_only=0):
     """Random-action games with re-create on termination (each new game from
-    the next config of generate_configs) for about ``seconds``; returns
-    (env-steps, elapsed)."""
+    the next config of generate_configs, filtered to ``planets_only``-planet
+    games when set, as BatchedEnv(planets_only=...)) for about ``seconds``;
+    returns (env-steps, elapsed)."""
     g = Game(config)
     rng = np.random.RandomState(seed)
-    seeds = np.random.RandomState(config.seed + seed)   # generate_configs stream
+    stream = np.random.RandomState(config.seed + seed)   # generate_configs stream
+
+    class _Seeds:
+        @staticmethod
+        def randint(hi):
+            while True:
+                s = stream.randint(hi)
+                if not planets_only or np.random.RandomState(s).randint(1, config.max_planets + 1) == planets_only:
+                    return s
+    seeds = _Seeds
     state = g.create(seeds.randint(1 << 30))
     steps = 0
     t0 = time.perf_counter()

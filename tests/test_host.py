@@ -167,3 +167,17 @@ def test_kernel_choice_mirrors_header():
     hdr = open(os.path.join(os.path.dirname(__graft_entry__.__file__), 'include', 'astro_step.h')).read()
     n = int(re.search(r'#define ASTRO_QUAD_MAX_ENVS (\d+)', hdr).group(1))
     assert _env.QUAD_MAX_ENVS == n
+
+
+def test_filtered_stream_oracle_matches_numpy():
+    """oracle.batched.filtered_game_seeds == config.generate_configs_filtered
+    (numpy RandomState draws create()'s planet count, core.py:90)."""
+    import itertools
+    from oracle import batched
+    from astro_amd.config import generate_configs_filtered
+    ss = batched.stream_seeds(42, 4)
+    got = batched.filtered_game_seeds(ss, 6, 3, 4)
+    for i in range(4):
+        want = [c.seed for c in itertools.islice(
+            generate_configs_filtered(DEFAULT_CONFIG._replace(seed=int(ss[i])), 3), 6)]
+        assert list(got[i]) == want

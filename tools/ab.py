@@ -26,7 +26,7 @@ def make(spec, wl, n, ticks, rollout):
     _lib.load(os.path.join(ROOT, 'astro_amd', lib + '.so'))
     w = bench.WORKLOADS[wl]
     env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=w['b_cap'],
-                     p_pad=w['p_pad'], auto_reset=True, kernel=kernel or 'auto')
+                     p_pad=w['p_pad'], auto_reset=True, kernel=kernel or 'auto', planets_only=w['planets_only'])
     env.reset()
     ctl = torch.from_numpy(bench.controls(0, n, env.S, ticks)).cuda()
     for t in range(50):

@@ -23,7 +23,7 @@ a = ap.parse_args()
 _lib.load(os.path.join(ROOT, 'astro_amd', a.lib + '.so'))
 w = bench.WORKLOADS[a.workload]
 env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), w['n'], device='cuda:0', b_cap=w['b_cap'],
-                 p_pad=w['p_pad'], auto_reset=not a.noreset)
+                 p_pad=w['p_pad'], auto_reset=not a.noreset, planets_only=w['planets_only'])
 env.reset()
 ctl = torch.from_numpy(bench.controls(0, w['n'], env.S, a.ticks)).cuda()
 for t in range(a.ticks):
