@@ -181,3 +181,14 @@ def test_filtered_stream_oracle_matches_numpy():
         want = [c.seed for c in itertools.islice(
             generate_configs_filtered(DEFAULT_CONFIG._replace(seed=int(ss[i])), 3), 6)]
         assert list(got[i]) == want
+
+
+def test_planets_only_validation():
+    """planets_only needs 1 <= P <= max_planets and max_planets a power of two
+    (one MT word decides create()'s count); checked before any device work."""
+    import pytest as _pytest
+    from astro_amd import BatchedEnv
+    with _pytest.raises(ValueError):
+        BatchedEnv(DEFAULT_CONFIG._replace(max_planets=3), 4, device='cuda:0', planets_only=2)
+    with _pytest.raises(ValueError):
+        BatchedEnv(DEFAULT_CONFIG, 4, device='cuda:0', planets_only=5)
