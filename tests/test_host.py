@@ -73,6 +73,15 @@ def test_argument_validation_without_gpu(lib):
     rc = lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None)
     assert rc == -13
     p.p_pad = 4
+    p.planets_only = 5   # > max_planets
+    assert lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None) == -19
+    p.max_planets, p.planets_only = 3, 2   # max_planets not a power of two
+    assert lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None) == -19
+    assert b'power of two' in lib.astro_last_error()
+    p.max_planets, p.planets_only = 4, 0
+    p.kernel = 4
+    assert lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None) == -18
+    p.kernel = 0
     s.n_env = -1
     assert lib.astro_reset(ctypes.byref(p), ctypes.byref(s), None, None, None) == -3
     s.n_env = 0   # empty batch: a no-op that never touches the device
