@@ -9,8 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 10
-READY_STRIDE = 640   # include/astro_step.h ASTRO_READY_STRIDE
+ABI_VERSION = 9
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'reserved')
@@ -59,8 +58,6 @@ class AstroState(ctypes.Structure):
         ('stream', ctypes.c_void_p),
         ('n_env', ctypes.c_int32),
         ('state_f64', ctypes.c_int32),
-        ('ready', ctypes.c_void_p),
-        ('ready_flag', ctypes.c_void_p),
     ]
 
 

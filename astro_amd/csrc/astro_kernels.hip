@@ -1244,8 +1244,7 @@ __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off,
 // row must be active; `write` gates the stores.
 template <typename T, int S, int PMAX>
 __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroState &st, int ie,
-                                              const CreateDraws<S> &d, int u, int row0, bool write,
-                                              char *rr = nullptr) {
+                                              const CreateDraws<S> &d, int u, int row0, bool write) {
     static_assert(2 * PMAX + 1 <= 16, "one angle per lane of a 16-lane row");
     using V = typename Store<T>::V;
     const size_t N = size_t(st.n_env);
@@ -1288,13 +1287,8 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
         v.y = T(sy);
         v.z = T(0);
         v.w = T(0);
-        if (rr) {   // a ready record (see ready_game): ships, bearings, planets
-            reinterpret_cast<V *>(rr)[u] = v;
-            reinterpret_cast<T *>(reinterpret_cast<V *>(rr) + S)[u] = T(b);
-        } else {
-            reinterpret_cast<V *>(st.ships)[size_t(u) * N + ie] = v;
-            reinterpret_cast<T *>(st.ships_b)[size_t(u) * N + ie] = T(b);
-        }
+        reinterpret_cast<V *>(st.ships)[size_t(u) * N + ie] = v;
+        reinterpret_cast<T *>(st.ships_b)[size_t(u) * N + ie] = T(b);
     }
     // planets (core.py:111-121): lane j < n writes planet j
     if (write && u < PMAX) {
@@ -1308,10 +1302,7 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
             v.z = T(amp * double(vs));
             v.w = T(amp * double(vc));
         }
-        if (u < n) {
-            if (rr) reinterpret_cast<V *>(rr)[S + 1 + u] = v;
-            else reinterpret_cast<V *>(st.planets)[size_t(u) * N + ie] = v;
-        }
+        if (u < n) reinterpret_cast<V *>(st.planets)[size_t(u) * N + ie] = v;
     }
     if (n > PMAX) n = PMAX;
     return n;
@@ -1328,12 +1319,11 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
 // then runs spread over the row (ship u, planet u).  An env whose first
 // randint word is rejected is flagged in s_serial for the quad's serial
 // create.  Returns the leaders not yet served.
-template <typename T, int S, int PMAX, int LPE, bool READY = false>
+template <typename T, int S, int PMAX, int LPE>
 __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
                                                     int lane, int i, uint32_t pend_seed, uint32_t pend_key,
                                                     bool have_key, uint32_t (*s_chain)[2][13 + 2 * S],
                                                     int *s_serial) {
-    using V = typename Store<T>::V;
     constexpr int NW = 12 + 2 * S;   // outputs create() draws, randint accepting its first word
     int leader[4];
 #pragma unroll
@@ -1401,11 +1391,9 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     d.exhausted = false;   // NW outputs, far below the 227 the lazy generator covers
 
     int n, cf = 0;
-    char *rr = READY ? static_cast<char *>(st.ready) + size_t(ie) * ASTRO_READY_STRIDE : nullptr;
     if constexpr (2 * PMAX + 1 <= 16) {
-        n = create_env_row<T, S, PMAX>(p, st, ie, d, u, row0, on && fast, rr);
+        n = create_env_row<T, S, PMAX>(p, st, ie, d, u, row0, on && fast);
     } else {
-        static_assert(!READY, "ready records need 2 PMAX + 1 <= 16");
         if (on && fast) n = create_env<T, S, PMAX, 16>(p, st, ie, d, cf, u);
     }
     if (on && fast) {
@@ -1416,67 +1404,12 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
             g.i = c.z;
             const bool exhausted = !g.ok();
             const uint32_t next_seed = g.next() & SEED_MASK;
-            const int hy = n | ((exhausted || cf) ? 2 << 8 : 0);
-            if (READY) {   // the record's tail; ready at the NEXT launch (flag 2 -> 1 there)
-                uint4 *meta = reinterpret_cast<uint4 *>(rr + (S + 1 + PMAX) * sizeof(V));
-                meta[0] = make_uint4(seed, uint32_t(hy), next_seed, 0u);
-                meta[1] = make_uint4(g.a, g.b, g.i, 0u);
-                st.ready_flag[ie] = 2;
-            } else {
-                reinterpret_cast<uint4 *>(st.stream)[ie] = make_uint4(g.a, g.b, g.i, seed);
-                reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, hy, int(next_seed), 0);
-            }
+            reinterpret_cast<uint4 *>(st.stream)[ie] = make_uint4(g.a, g.b, g.i, seed);
+            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | ((exhausted || cf) ? 2 << 8 : 0), int(next_seed), 0);
         }
     }
-    if (!READY && on && !fast && u == 0) s_serial[L / LPE] = 1;
+    if (on && !fast && u == 0) s_serial[L / LPE] = 1;
     return todo;
-}
-
-// Ready games (AstroState.ready): creator waves appended to astro_step's grid
-// make each env's NEXT game ahead of time, so that the step's auto-reset
-// copies a record instead of running a reset pass on the launch's critical
-// path.  Creator wave cw looks after envs [128 cw, 128 cw + 128): it promotes
-// the records the previous launch wrote (flag 2 -> 1: readable from now on,
-// never written in the launch that reads it) and makes the next game of up to
-// four envs whose record is empty and whose pending seed is settled
-// (KEY_VALID: key[397] gathered, planets_only checked) -- one reset pass,
-// writing the record.  A step that finds its env's record readable and
-// tagged with its pending seed copies it; a stale record (the pending seed
-// moved on) is dropped.
-constexpr int READY_BLOCK = 128;
-
-template <typename T, int S, int PMAX>
-__device__ void ready_wave(const AstroParams &p, const AstroState &st, int cw) {
-    __shared__ uint32_t s_chain_all[QW][4][2][13 + 2 * S];
-    __shared__ int s_serial_all[QW][16];
-    const int wv = QW == 1 ? 0 : int(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int N = st.n_env;
-    int e[2];
-    bool cand[2];
-    uint32_t seed[2], key[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        e[k] = cw * READY_BLOCK + 64 * k + lane;
-        const bool v = e[k] < N;
-        const int f = v ? int(st.ready_flag[e[k]]) : 1;
-        const int4 h = v ? reinterpret_cast<const int4 *>(st.hdr)[e[k]] : make_int4(0, 0, 0, 0);
-        if (v && f == 2) st.ready_flag[e[k]] = 1;
-        cand[k] = v && f == 0 && (uint32_t(h.x) & KEY_VALID) != 0;
-        seed[k] = uint32_t(h.z);
-        key[k] = uint32_t(h.w);
-    }
-    const uint64_t m0 = __ballot(cand[0]), m1 = __ballot(cand[1]);
-    const bool second = m0 == 0;   // uniform
-    uint64_t todo = second ? m1 : m0, take = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {   // at most one pass per launch
-        take |= todo & (~todo + 1);
-        todo &= todo ? todo - 1 : 0;
-    }
-    if (!take) return;
-    wave_reset_pass<T, S, PMAX, 4, true>(p, st, take, lane, second ? e[1] : e[0], second ? seed[1] : seed[0],
-                                         second ? key[1] : key[0], true, s_chain_all[wv], s_serial_all[wv]);
 }
 
 // Counters one tick of a quad-kernel wave adds to its stats row.
@@ -1594,10 +1527,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // waits for, so only its consumers (header store, reset) wait for it
     if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
     uint4 c_pend = make_uint4(0u, 0u, 0u, 0u);   // stream cursor, for check_pending
-    // a ready-made next game (see ready_wave): readable when its flag is 1
-    constexpr bool READY_OK = 2 * PMAX + 1 <= 16;
-    const bool ready_on = READY_OK && st.ready != nullptr;   // uniform
-    const int rflag = ready_on && q == 0 ? int(st.ready_flag[i]) : 0;
     if (q == 0 && !key_valid && p.key_table && p.planets_only) c_pend = reinterpret_cast<const uint4 *>(st.stream)[i];
 
     // ---- quad broadcasts: all planets, both ships
@@ -2032,38 +1961,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         }
     }
 
-    // ---- ready games: a finished env whose record is readable and made from
-    //      its pending seed takes it (copies), instead of a reset pass
-    if (ready_on && __any(need_reset && rflag == 1)) {
-        if (quad_any<LPE>(need_reset && rflag == 1, lane)) {   // uniform over the group
-            const char *rr = static_cast<const char *>(st.ready) + size_t(is) * ASTRO_READY_STRIDE;
-            const uint4 *meta = reinterpret_cast<const uint4 *>(rr + (S + 1 + PMAX) * sizeof(V));
-            const uint4 m0 = meta[0], m1 = meta[1];
-            const V shv = reinterpret_cast<const V *>(rr)[sq];
-            const T bv = reinterpret_cast<const T *>(reinterpret_cast<const V *>(rr) + S)[sq];
-            V plv[PPL];
-#pragma unroll
-            for (int m = 0; m < PPL; ++m) plv[m] = reinterpret_cast<const V *>(rr)[S + 1 + q + LPE * m];
-            const bool ok = m0.x == pend_seed;   // (uniform over the group)
-            if (ok) {
-                const int n = int(m0.y & 0xffu);
-                if (q < S) {
-                    ships[size_t(q) * NN + is] = shv;
-                    ships_b[size_t(q) * NN + is] = bv;
-                }
-#pragma unroll
-                for (int m = 0; m < PPL; ++m)
-                    if (q + LPE * m < n) planets[size_t(q + LPE * m) * NN + is] = plv[m];
-                if (q == 0) {
-                    reinterpret_cast<uint4 *>(st.stream)[is] = make_uint4(m1.x, m1.y, m1.z, m0.x);
-                    reinterpret_cast<int4 *>(st.hdr)[is] = make_int4(0, int(m0.y), int(m0.z), 0);
-                }
-            }
-            if (q == 0) st.ready_flag[is] = 0;
-            need_reset = need_reset && !ok;
-        }
-    }
-
     // ---- auto-reset: the wave creates its finished envs' next games together,
     //      up to four per pass with 16 lanes each (wave_reset_pass); rejected
     //      randint words (max_planets not a power of two) take the serial path
@@ -2155,14 +2052,6 @@ __global__ __launch_bounds__(QBLOCK, MULTI ? 2 : 4) void astro_step_quad_kernel(
     //      grid-wide barrier between ticks (envs never interact); the
     //      counters go to the wave's stats row after every tick, so nothing
     //      but the tick number lives across the loop
-    const int step_blocks = int(((int64_t(st.n_env) * LPE + 63) / 64 + QW - 1) / QW);
-    if (int(blockIdx.x) >= step_blocks) {   // creator waves (ready games), appended to the grid
-        if constexpr (!MULTI && 2 * PMAX + 1 <= 16) {
-            const int cw = (int(blockIdx.x) - step_blocks) * QW + int(threadIdx.x >> 6);
-            if (st.ready && cw * READY_BLOCK < st.n_env) ready_wave<T, S, PMAX>(p, st, cw);
-        }
-        return;
-    }
     if (int(blockIdx.x * QW + threadIdx.x / 64) * (64 / LPE) >= st.n_env) return;   // a spare wave of the last block
     const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
     for (int kt = 0; kt < n_ticks; ++kt) {
@@ -2382,9 +2271,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
     const int kind = pick_kernel(p, s.n_env);
     if (kind == ASTRO_KERNEL_QUAD || kind == ASTRO_KERNEL_PAIR) {   // all ticks in one launch
         const int lpe = kind == ASTRO_KERNEL_QUAD ? 4 : 2;
-        int grid = int((int64_t(s.n_env) * lpe + QBLOCK - 1) / QBLOCK);
-        if (s.ready && drv.ticks == 1 && 2 * PM + 1 <= 16)   // + the creator waves of ready games
-            grid += int(((int64_t(s.n_env) + READY_BLOCK - 1) / READY_BLOCK + QW - 1) / QW);
+        const int grid = int((int64_t(s.n_env) * lpe + QBLOCK - 1) / QBLOCK);
         if (lpe == 4 && drv.ticks == 1)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);

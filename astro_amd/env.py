@@ -85,14 +85,11 @@ class BatchedEnv:
                   filtered to the seeds whose create() draws exactly P planets
                   (config.generate_configs_filtered); max_planets must be a
                   power of two
-    ready_games -- let astro_step's background waves make each env's next
-                  game ahead (AstroState.ready, 640 B per env), so an
-                  auto-reset copies it; same results either way
     """
 
     def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
                  dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto',
-                 use_key_table=True, planets_only=0, ready_games=True):
+                 use_key_table=True, planets_only=0):
         _schedule.check_config(config)
         planets_only = int(planets_only)
         if planets_only and (not 1 <= planets_only <= config.max_planets
@@ -128,8 +125,6 @@ class BatchedEnv:
         self.reward = z(N, S, dt=torch.float32)
         self.done = z(N, dt=torch.uint8)
         self.stats = z(max(1, (N + 15) // 16), _lib.NSTATS, dt=torch.int64)
-        self.ready = z(N, _lib.READY_STRIDE, dt=torch.uint8) if ready_games else None
-        self.ready_flag = z(N, dt=torch.uint8) if ready_games else None
         self.fire_bits = torch.from_numpy(self.schedule.fire_bits().view(np.int32)).to(dev)
 
         k = _schedule.kernel_constants(config)
@@ -142,9 +137,7 @@ class BatchedEnv:
             ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),
             planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),
             hdr=self.hdr.data_ptr(), stream=self.stream.data_ptr(),
-            n_env=N, state_f64=1 if dtype == torch.float64 else 0,
-            ready=self.ready.data_ptr() if ready_games else None,
-            ready_flag=self.ready_flag.data_ptr() if ready_games else None)
+            n_env=N, state_f64=1 if dtype == torch.float64 else 0)
 
         self.stream_seeds = _shard.stream_seeds(config, self.env_offset, N)
         seeds_t = torch.from_numpy(self.stream_seeds.view(np.int32)).to(dev)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 10
+#define ASTRO_ABI_VERSION 9
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -104,15 +104,7 @@ typedef struct AstroState {
     uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, current game's seed */
     int32_t n_env;
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
-    void *ready;        /* optional [n_env][ASTRO_READY_STRIDE] bytes: each env's NEXT game,
-                           made ahead by background waves of astro_step (QUAD/PAIR kernels,
-                           p_pad <= 7) so that an auto-reset copies instead of creating;
-                           NULL = create at the reset.  Results are identical either way. */
-    uint8_t *ready_flag;/* [n_env], zero-initialised: 0 empty, 2 written by the running
-                           launch, 1 readable (promoted by the next launch) */
 } AstroState;
-
-#define ASTRO_READY_STRIDE 640
 
 /* Control sources of astro_rollout. */
 enum {

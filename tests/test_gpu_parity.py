@@ -122,32 +122,6 @@ def test_planets_only_streams(kernel):
     assert games.max() > 2
 
 
-@pytest.mark.parametrize('kernel', ['quad', 'pair'])
-@pytest.mark.parametrize('planets_only', [0, 3])
-def test_ready_games_identical(kernel, planets_only):
-    """Games made ahead by astro_step's creator waves (AstroState.ready) are
-    the games a reset pass makes: with and without them every state array is
-    equal after 300 ticks with thousands of resets, and records were made."""
-    from astro_amd import BatchedEnv
-    cfg = CFG['default']
-    n, ticks = 8192, 300
-    g = torch.Generator(device='cuda').manual_seed(7)
-    ctls = torch.randint(0, 6, (ticks, n, 2), generator=g, device='cuda', dtype=torch.int8)
-    envs = [BatchedEnv(cfg, n, device='cuda:0', kernel=kernel, planets_only=planets_only, ready_games=r)
-            for r in (True, False)]
-    made = 0
-    for e in envs:
-        e.reset()
-        for t in range(ticks):
-            e.step(ctls[t])
-            if e.ready is not None and t % 50 == 49:
-                made += int((e.ready_flag != 0).sum())
-    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
-        assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), f
-    assert envs[0].stat_dict() == envs[1].stat_dict()
-    assert envs[0].stat_dict()['resets'] > 1000 and made > 1000
-
-
 # ------------------------------------------------- teacher-forced transitions
 
 @pytest.mark.parametrize('kernel', KERNELS)
