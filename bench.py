@@ -275,6 +275,21 @@ def main():
                 tj = json.load(f)
             if tj.get('n_env') == n and tj.get('kernel') in (args.kernel, 'auto'):
                 traffic = tj.get('hbm_bytes_per_launch')
+        # secondary bound: VALU issue, from the committed PMC instruction count
+        # of this workload's kernel (profiles/round1/pmc_<workload>_<state>.json)
+        issue = None
+        ppath = os.path.join(ROOT, 'profiles', 'round1', 'pmc_%s_%s.json' % (args.workload, args.state))
+        if os.path.exists(ppath):
+            with open(ppath) as f:
+                pj = json.load(f)
+            lpe = dict(lane=1, quad=4, pair=2)[env.step_kernel]
+            if pj.get('n_env') == n and pj.get('lanes_per_env') == lpe:
+                rate = pj['waves'] * pj['valu_per_wave'] / (launch_ms * 1e-3)
+                peak = 256 * 4 * 2.4e9 / 4
+                issue = dict(bound='valu-issue', achieved=rate, peak=peak, unit='wave-instructions/s',
+                             frac=rate / peak, valu_per_wave=pj['valu_per_wave'], waves=pj['waves'],
+                             note='not HBM-bound and not issue-bound: two waves per SIMD at c3, '
+                                  'latency-bound (DESIGN.md section 3)')
         out = dict(
             metric=METRIC, value=value, unit='env-steps/s', n_gpus=world, steps=args.steps,
             warmup=args.warmup, ms_per_step=wall_max / args.steps * 1e3, higher_is_better=True,
@@ -291,6 +306,7 @@ def main():
                           kernel=('astro_step_kernel' if env.step_kernel == 'lane' else 'astro_step_quad_kernel'),
                           lanes_per_env=dict(lane=1, quad=4, pair=2)[env.step_kernel],
                           timing='hipEvent pair around the timed region / K launches'),
+            issue_roofline=issue,
             gpu_ms_per_step=gpu_ms_per_step,
             timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph
                                               if args.graph else 'eager'),
