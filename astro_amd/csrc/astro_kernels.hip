@@ -1228,12 +1228,17 @@ __device__ __forceinline__ uint32_t bw_tag(int e, int np, bool t0) {
 
 // Index window [w0, w0 + QWIN) of the wave's live bullets: the group of an
 // env whose bullets are numbered off .. off + nb - 1 writes the words of
-// those in the window, lane q taking slots k = q mod LPE.
+// those in the window, lane q a contiguous run of ceil(nb / LPE) slots (the
+// word of slot k + 1 is the word of slot k plus 1 << 5: an add and an LDS
+// store per slot; the last slot's flag is OR-ed in after the loop).
 template <int LPE>
 __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off, int nb, int q, uint32_t tag) {
-    const int lo = max(0, w0 - off), hi = min(nb, w0 + QWIN - off);
-    for (int k = lo + ((q - lo) & (LPE - 1)); k < hi; k += LPE)
-        s_index[off + k - w0] = tag | (uint32_t(k) << 5) | (k == nb - 1 ? 1u << 21 : 0u);
+    const int h = (nb + LPE - 1) / LPE;
+    const int k0 = max(q * h, w0 - off), k1 = min(min(nb, (q + 1) * h), w0 + QWIN - off);
+    uint32_t w = tag | (uint32_t(k0) << 5);
+    uint32_t *dst = s_index + (off + k0 - w0);
+    for (int k = k0; k < k1; ++k, w += 1u << 5) *dst++ = w;
+    if (k1 == nb && k1 > k0) dst[-1] = w - (1u << 5) + (1u << 21);   // last of the env
 }
 
 // create() of one env spread over a row of 16 lanes, for PMAX <= 7: each
