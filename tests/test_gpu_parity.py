@@ -89,18 +89,23 @@ def test_seed_streams_follow_generate_configs():
 
 
 @pytest.mark.parametrize('kernel', KERNELS)
-def test_planets_only_streams(kernel):
+@pytest.mark.parametrize('fast_end', [False, True])
+def test_planets_only_streams(kernel, fast_end):
     """planets_only=3 (BASELINE.json's "3 planets" workloads): every game an
     env plays, through reset() and auto-reset alike, is the next seed of its
     generate_configs stream whose create() draws 3 planets, and the game is
-    that seed's reference game (bit-exact vs the oracle's create + step)."""
+    that seed's reference game (bit-exact vs the oracle's create + step).
+    fast_end: huge planets end most games at their first step, before any
+    step has checked the next pending seed -- the resets' own seed walk."""
     cfg = CFG['default']
+    if fast_end:
+        cfg = cfg._replace(planet_radius=0.45)
     P = batched.make_params(cfg)
-    n, ticks = 1000, 150
+    n, ticks = 1000, 150 if not fast_end else 25
     from astro_amd import BatchedEnv
     env = BatchedEnv(cfg, n, device='cuda:0', b_cap=32, planets_only=3, kernel=kernel)
     env.reset()
-    seeds = batched.filtered_game_seeds(env.stream_seeds, 12, 3, cfg.max_planets)
+    seeds = batched.filtered_game_seeds(env.stream_seeds, 12 if not fast_end else 30, 3, cfg.max_planets, draws=220)
     assert (env.game_seed.cpu().numpy().view(np.uint32) == seeds[:, 0]).all()
     games = np.ones(n, np.int64)
     rng = np.random.RandomState(2)
