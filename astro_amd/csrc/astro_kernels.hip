@@ -191,6 +191,19 @@ __device__ __forceinline__ bool near32(float ax, float ay, float bx, float by, c
     return d2 < g.lo;
 }
 
+// The same test on a lane that may be at tick 0: there the reference's own
+// distance IS this float32 one (create()'s float32 arrays; closer_exact's
+// float(a) - float(b) of the same values, no fma), so tick 0 is decided here
+// against the largest float below r^2 and never goes to the exact path.
+__device__ __forceinline__ bool near32_t0(float ax, float ay, float bx, float by, const Guard &g, bool &amb,
+                                          bool t0) {
+    const float dx = ax - bx;
+    const float dy = ay - by;
+    const float d2 = dx * dx + dy * dy;
+    amb |= !t0 & (d2 >= g.lo) & (d2 <= g.hi);
+    return t0 ? d2 <= g.t0_max : d2 < g.lo;
+}
+
 // the exact test of the ambiguous path: at tick 0 the float32 distance of
 // create()'s float32 arrays, later float64
 __device__ __forceinline__ bool closer_exact(double ax, double ay, double bx, double by, const Guard &g, bool t0) {
@@ -948,7 +961,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 #ifdef ASTRO_COLLIDE_F64
             amb = true;
 #endif
-            if (__any(amb)) {   // the exact tests, for the ambiguous and tick-0 lanes
+            if (__any(amb)) {   // the exact tests, for the ambiguous lanes (never tick 0, see near32_t0)
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     bool hs = false;
@@ -1598,13 +1611,12 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         for (int s = 0; s < S; ++s) {
             bool hs = false;
 #pragma unroll
-            for (int m = 0; m < PPL; ++m) hs |= near32(sxf[s], syf[s], mpxf[m], mpyf[m], gsp, amb);
+            for (int m = 0; m < PPL; ++m) hs |= near32_t0(sxf[s], syf[s], mpxf[m], mpyf[m], gsp, amb, t0);
             hsp[s] = hs;
         }
         bool hh = false;
-        if (S == 2 && q == 0) hh = near32(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, amb);
-        amb |= t0;
-        if (__any(amb)) {   // the exact tests, for the ambiguous and tick-0 lanes
+        if (S == 2 && q == 0) hh = near32_t0(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, amb, t0);
+        if (__any(amb)) {   // the exact tests, for the ambiguous lanes (never tick 0, see near32_t0)
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 bool hs = false;
