@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
 ABI_VERSION = 9
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
-              'overflows', 'planets', 'reserved')
+              'overflows', 'planets', 'serial_resets')
 NSTATS = 8
 KERNELS = {'auto': 0, 'lane': 1, 'quad': 2, 'pair': 3}
 

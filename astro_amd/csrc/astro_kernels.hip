@@ -1434,6 +1434,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
 struct QuadCounts {
     uint32_t n_bin, n_bout, n_pl, n_drop;   // per lane
     uint32_t c_reset, c_coll, c_tout;       // per wave
+    uint32_t c_serial;                      // per wave: resets by the serial create
 };
 
 #ifdef ASTRO_STAMPS
@@ -1479,7 +1480,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     V *planets = reinterpret_cast<V *>(st.planets);
     V *bullets = reinterpret_cast<V *>(st.bullets);
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;   // per lane, summed over the launch's ticks
-    uint32_t c_reset = 0, c_coll = 0, c_tout = 0;           // per wave
+    uint32_t c_reset = 0, c_coll = 0, c_tout = 0, c_serial = 0;           // per wave
     const int sq = q < S ? q : 0;
     float *__restrict__ reward = reward_all + size_t(kt) * NN * S;
     uint8_t *__restrict__ done_out = done_all + size_t(kt) * NN;
@@ -1986,6 +1987,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                                            s_chain, s_serial);
     if (auto_reset) {
         wave_sync();
+        if (stats) c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));
         if (active && s_serial[e]) {   // uniform over the quad; rare
             const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(pend_key)));   // lane q == 0 fetched it
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
@@ -2010,7 +2012,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         stamp_[15] = n_res | (n_t0 << 8) | ((unsigned long long)total << 16);
     }
 #endif
-    return QuadCounts{n_bin, n_bout, n_pl, n_drop, c_reset, c_coll, c_tout};
+    return QuadCounts{n_bin, n_bout, n_pl, n_drop, c_reset, c_coll, c_tout, c_serial};
 }
 
 // Add one tick's counters to the wave's private stats row (lane 0).  A
@@ -2033,6 +2035,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long *slot, const Qua
         if (c.c_tout) atomicAdd(slot + ASTRO_STAT_TIMEOUTS, (unsigned long long)c.c_tout);
         if (drop) atomicAdd(slot + ASTRO_STAT_OVERFLOWS, (unsigned long long)drop);
         if (pl) atomicAdd(slot + ASTRO_STAT_PLANETS, (unsigned long long)pl);
+        if (c.c_serial) atomicAdd(slot + ASTRO_STAT_SERIAL, (unsigned long long)c.c_serial);
     }
 }
 

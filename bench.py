@@ -311,6 +311,7 @@ def main():
             timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph
                                               if args.graph else 'eager'),
             stats=dict(mean_live_bullets=tot[0] / (n_total * args.steps),
+                       serial_resets_per_step=d.get('serial_resets', 0) / args.steps,
                        resets_per_step=tot[1] / args.steps, overflow_bullets=tot[2],
                        collisions=tot[3], timeouts=tot[4],
                        mean_planets=d['planets'] / (n * args.steps)),

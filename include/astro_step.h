@@ -135,6 +135,8 @@ enum {
     ASTRO_STAT_TIMEOUTS = 4,    /* games ended by max_time */
     ASTRO_STAT_OVERFLOWS = 5,   /* bullets dropped for lack of b_cap */
     ASTRO_STAT_PLANETS = 6,     /* planet slots read */
+    ASTRO_STAT_SERIAL = 7,      /* resets the QUAD/PAIR kernels could not make in their
+                                   wave-cooperative pass (serial create) */
     ASTRO_NSTATS = 8
 };
 
