@@ -2116,47 +2116,91 @@ __device__ __forceinline__ C norm_angle_over_pi(C b) {
     return (m - pi) / pi;
 }
 
+// A block covers 256 consecutive (env, row) items: the per-env part (every
+// ship's five features, with norm_angle's exact fmod) is computed once per
+// env into LDS rather than once per row, and the block's 256 x D floats go out
+// through LDS as coalesced 16-byte stores (a lane per item storing its own D
+// floats wrote 4-byte words 60 bytes apart).
+constexpr int FEAT_BLOCK = 256;
+
 template <typename T, int S>
-__global__ __launch_bounds__(256) void astro_features_kernel(AstroParams p, AstroState st, float *__restrict__ out,
-                                                             int rows) {
+__global__ __launch_bounds__(FEAT_BLOCK) void astro_features_kernel(AstroParams p, AstroState st,
+                                                                   float *__restrict__ out, int rows) {
     using V = typename Store<T>::V;
     constexpr int D = 1 + 5 * S + 4;
-    const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    constexpr int MAXE = FEAT_BLOCK + 1;   // envs a block can touch (rows >= 1)
+    __shared__ float s_ship[MAXE][5 * S];
+    __shared__ int s_cnt[MAXE][2];         // nplanets, nbullets
+    __shared__ float4 s_out[FEAT_BLOCK * D / 4 + 1];
     const int N = st.n_env;
-    if (idx >= int64_t(N) * rows) return;
-    const int i = int(idx / rows), r = int(idx - int64_t(i) * rows);
     const size_t NN = size_t(N);
-    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
-    int np = h.y & 0xff;
-    np = np < 1 ? 1 : (np > p.p_pad ? p.p_pad : np);
-    const int nb = min(int(uint32_t(h.y) >> 16), p.b_cap);
-    const bool t0 = (uint32_t(h.x) & TICK_MASK) == 0;
-    float f[D];
-    if (r >= np + nb) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) f[k] = -1.0f;   // to_batch padding
-    } else {
-        f[0] = r < np ? 0.0f : 1.0f;
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const V v = reinterpret_cast<const V *>(st.ships)[size_t(s) * NN + i];
-            const T b = reinterpret_cast<const T *>(st.ships_b)[size_t(s) * NN + i];
-            f[1 + 5 * s] = float(v.x);
-            f[2 + 5 * s] = float(v.y);
-            f[3 + 5 * s] = float(v.z);
-            f[4 + 5 * s] = float(v.w);
-            f[5 + 5 * s] = t0 ? norm_angle_over_pi<float>(float(b)) : float(norm_angle_over_pi<double>(double(b)));
+    const int64_t total = int64_t(N) * rows;
+    const int64_t b0 = int64_t(blockIdx.x) * FEAT_BLOCK;
+    const int64_t b1 = min(total, b0 + FEAT_BLOCK);   // items [b0, b1)
+    const int e0 = int(b0 / rows), ne = int((b1 - 1) / rows) - e0 + 1;
+    const int t = threadIdx.x;
+
+    // per env: counts and the ships' features (float32 for create()'s float32
+    // ships at tick 0, float64 after, as numpy)
+    for (int k = t; k < ne * S; k += FEAT_BLOCK) {
+        const int le = k / S, s = k - le * S, i = e0 + le;
+        const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+        if (s == 0) {
+            int np = h.y & 0xff;
+            s_cnt[le][0] = np < 1 ? 1 : (np > p.p_pad ? p.p_pad : np);
+            s_cnt[le][1] = min(int(uint32_t(h.y) >> 16), p.b_cap);
         }
-        const V o = r < np ? reinterpret_cast<const V *>(st.planets)[size_t(r) * NN + i]
-                           : reinterpret_cast<const V *>(st.bullets)[size_t(i) * size_t(p.b_cap) + (r - np)];
-        f[1 + 5 * S] = float(o.x);
-        f[2 + 5 * S] = float(o.y);
-        f[3 + 5 * S] = float(o.z);
-        f[4 + 5 * S] = float(o.w);
+        const bool t0 = (uint32_t(h.x) & TICK_MASK) == 0;
+        const V v = reinterpret_cast<const V *>(st.ships)[size_t(s) * NN + i];
+        const T b = reinterpret_cast<const T *>(st.ships_b)[size_t(s) * NN + i];
+        float *f = s_ship[le] + 5 * s;
+        f[0] = float(v.x);
+        f[1] = float(v.y);
+        f[2] = float(v.z);
+        f[3] = float(v.w);
+        f[4] = t0 ? norm_angle_over_pi<float>(float(b)) : float(norm_angle_over_pi<double>(double(b)));
     }
-    float *dst = out + idx * D;
+    __syncthreads();
+
+    // per item: its row
+    const int64_t idx = b0 + t;
+    if (idx < b1) {
+        const int i = int(idx / rows), r = int(idx - int64_t(i) * rows), le = i - e0;
+        const int np = s_cnt[le][0], nb = s_cnt[le][1];
+        float f[D];
+        if (r >= np + nb) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) dst[k] = f[k];
+            for (int k = 0; k < D; ++k) f[k] = -1.0f;   // to_batch padding
+        } else {
+            f[0] = r < np ? 0.0f : 1.0f;
+#pragma unroll
+            for (int k = 0; k < 5 * S; ++k) f[1 + k] = s_ship[le][k];
+            const V o = r < np ? reinterpret_cast<const V *>(st.planets)[size_t(r) * NN + i]
+                               : reinterpret_cast<const V *>(st.bullets)[size_t(i) * size_t(p.b_cap) + (r - np)];
+            f[1 + 5 * S] = float(o.x);
+            f[2 + 5 * S] = float(o.y);
+            f[3 + 5 * S] = float(o.z);
+            f[4 + 5 * S] = float(o.w);
+        }
+        float *so = reinterpret_cast<float *>(s_out) + t * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) so[k] = f[k];
+    }
+    __syncthreads();
+
+    // the block's items out: floats [b0 D, b1 D), 16 bytes per lane and store
+    // where the block's base is 16-byte aligned (out is; b0 D floats is a
+    // multiple of 4 when D or FEAT_BLOCK is), else word by word
+    const int64_t nf = (b1 - b0) * D;
+    float *dst = out + b0 * D;
+    const float *src = reinterpret_cast<const float *>(s_out);
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        const int64_t n4 = nf / 4;
+        for (int64_t k = t; k < n4; k += FEAT_BLOCK) reinterpret_cast<float4 *>(dst)[k] = s_out[k];
+        for (int64_t k = n4 * 4 + t; k < nf; k += FEAT_BLOCK) dst[k] = src[k];
+    } else {
+        for (int64_t k = t; k < nf; k += FEAT_BLOCK) dst[k] = src[k];
+    }
 }
 
 template <typename T, int S, int PMAX>
@@ -2352,7 +2396,8 @@ template <typename T, int S, int PM>
 struct FeatL {   // (no PMAX dependence: one instance per T, S)
     static int run(const AstroParams &p, const AstroState &s, float *out, int rows, hipStream_t st) {
         const int64_t lanes = int64_t(s.n_env) * rows;
-        hipLaunchKernelGGL((astro_features_kernel<T, S>), dim3(unsigned((lanes + 255) / 256)), dim3(256), 0, st, p, s,
+        hipLaunchKernelGGL((astro_features_kernel<T, S>), dim3(unsigned((lanes + FEAT_BLOCK - 1) / FEAT_BLOCK)),
+                           dim3(FEAT_BLOCK), 0, st, p, s,
                            out, rows);
         return launched("astro_features");
     }
