@@ -2322,9 +2322,9 @@ int launched(const char *what) {
 // give the SIMDs more waves to hide latency with (16,384 envs: 8.7 us vs
 // 10.2 PAIR); 16 planet slots spill both, LANE.
 int pick_kernel(const AstroParams &p, int n_env) {
+    if (p.p_pad > 8) return ASTRO_KERNEL_LANE;   // (QUAD/PAIR are built for up to 8 planet slots)
     if (p.kernel == ASTRO_KERNEL_LANE || p.kernel == ASTRO_KERNEL_QUAD || p.kernel == ASTRO_KERNEL_PAIR)
         return p.kernel;
-    if (p.p_pad > 8) return ASTRO_KERNEL_LANE;
     return n_env <= ASTRO_QUAD_MAX_ENVS ? ASTRO_KERNEL_QUAD : ASTRO_KERNEL_PAIR;
 }
 
@@ -2333,6 +2333,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
                 uint64_t *stats, int ar, hipStream_t stream) {
     unsigned long long *st = reinterpret_cast<unsigned long long *>(stats);
     const int kind = pick_kernel(p, s.n_env);
+    if constexpr (PM <= 8)
     if (kind == ASTRO_KERNEL_QUAD || kind == ASTRO_KERNEL_PAIR) {   // all ticks in one launch
         const int lpe = kind == ASTRO_KERNEL_QUAD ? 4 : 2;
         const int grid = int((int64_t(s.n_env) * lpe + QBLOCK - 1) / QBLOCK);

@@ -196,6 +196,8 @@ class BatchedEnv:
         """'quad' or 'lane': the kernel astro_step runs for this env batch
         (the library's AUTO rule, pick_kernel in astro_kernels.hip)."""
         k = self.params.kernel
+        if self.p_pad > 8:
+            return 'lane'   # (QUAD/PAIR are built for up to 8 planet slots)
         for name in ('lane', 'quad', 'pair'):
             if k == _lib.KERNELS[name]:
                 return name

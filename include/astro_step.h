@@ -80,7 +80,8 @@ typedef struct AstroParams {
 /* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:
  * four lanes per env (16 envs per wave) for ships and planets, and the wave's
  * live bullets spread densely over its 64 lanes; PAIR: the same with two
- * lanes per env (32 envs per wave).  AUTO picks LANE for p_pad > 8, else
+ * lanes per env (32 envs per wave).  QUAD and PAIR exist for p_pad <= 8:
+ * larger p_pad always runs LANE.  AUTO picks LANE for p_pad > 8, else
  * QUAD for n_env <= ASTRO_QUAD_MAX_ENVS and PAIR above (measured crossover).
  * All give identical results. */
 enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2, ASTRO_KERNEL_PAIR = 3 };
