@@ -1183,6 +1183,14 @@ __device__ __forceinline__ void bcast_slots(const T (&mine)[PPL], double (&out)[
     }
 }
 
+// a double from the other lane of the caller's pair (quad_perm(1,0,3,2))
+__device__ __forceinline__ double pair_swap(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp(int(b & 0xffffffffll), 0xB1, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), 0xB1, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(uint32_t(lo)) | ((long long)hi << 32));
+}
+
 // OR of a per-lane flag over the lane's group (all group lanes must be active)
 template <int LPE = 4>
 __device__ __forceinline__ bool quad_any(bool f, int lane) {
@@ -1917,6 +1925,35 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 bcast_slots<T, PPL, LPE>(rx, px);
                 bcast_slots<T, PPL, LPE>(ry, py);
             }
+            // Pair kernel, 4 slots: the float64 planet-planet factors
+            // gm / max(1e-12, d2) of the 6 distinct pairs, 3 per lane (d2 and
+            // so the factor are the same bit for bit both ways round), the
+            // partner's two by DPP; row i of lane q's planets i = q, q + 2 is
+            // then F(i, j) for j = 0..3 (see symmetric_rows)
+            double Fr[PPL][PMAX];
+            if constexpr (LPE == 2 && PMAX == 4) {
+                const bool l0 = q == 0;
+                auto fac = [&](int i, int j) {
+                    const double ddx = px[j] - px[i], ddy = py[j] - py[i];
+                    return div_gravity(p.gm, max_floor(ddx * ddx + ddy * ddy));
+                };
+                // lane 0: A = F01, B = F03, C = F02; lane 1: A = F12, B = F23, C = F13
+                const double A = l0 ? fac(0, 1) : fac(1, 2);
+                const double B = l0 ? fac(0, 3) : fac(2, 3);
+                const double C = l0 ? fac(0, 2) : fac(1, 3);
+                const double A2 = pair_swap(A), B2 = pair_swap(B);   // lane 0: F12, F23; lane 1: F01, F03
+                const double z = 0.0;   // (self: unused)
+                // planet q:     lane 0 [-, F01, F02, F03]   lane 1 [F10, -, F12, F13]
+                // planet q + 2: lane 0 [F20, F21, -, F23]   lane 1 [F30, F31, F32, -]
+                Fr[0][0] = l0 ? z : A2;
+                Fr[0][1] = l0 ? A : z;
+                Fr[0][2] = l0 ? C : A;
+                Fr[0][3] = l0 ? B : C;
+                Fr[1][0] = l0 ? C : B2;
+                Fr[1][1] = l0 ? A2 : C;
+                Fr[1][2] = l0 ? z : B;
+                Fr[1][3] = l0 ? B2 : z;
+            }
 #pragma unroll
             for (int m = 0; m < PPL; ++m) {
                 const int j = q + LPE * m;
@@ -1946,7 +1983,30 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                             gx = px[1] - pxj;
                             gy = py[1] - pyj;
 #else
-                            field<double, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
+                            if constexpr (LPE == 2 && PMAX == 4) {
+                                // field<double> at planet j from the shared factors:
+                                // term k = F(j, k) * (p_k - p_j) summed in k order; the
+                                // self term is gm / 1e-12 * (+0), a zero with gm's sign
+                                const double zs = __builtin_signbit(p.gm) ? -0.0 : 0.0;
+                                double ax = 0.0, ay = 0.0;
+#pragma unroll
+                                for (int k = 0; k < PMAX; ++k) {
+                                    const bool self = k == j;
+                                    const double tx = self ? zs : Fr[m][k] * (px[k] - pxj);
+                                    const double ty = self ? zs : Fr[m][k] * (py[k] - pyj);
+                                    if (k == 0) {
+                                        ax = tx;
+                                        ay = ty;
+                                    } else {
+                                        ax = k < np ? ax + tx : ax;
+                                        ay = k < np ? ay + ty : ay;
+                                    }
+                                }
+                                gx = ax;
+                                gy = ay;
+                            } else {
+                                field<double, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
+                            }
 #endif
                             ndx = pdx + gx * p.dt;
                             ndy = pdy + gy * p.dt;
