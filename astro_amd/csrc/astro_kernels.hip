@@ -132,13 +132,15 @@ __device__ __forceinline__ C max_floor(C d2) {
 // field = gm / max(1e-12, |r|^2) * r  (a 1/r law in 2-D: no sqrt)
 template <typename C, int PMAX>
 __device__ __forceinline__ void field(const double (&px)[PMAX], const double (&py)[PMAX], int np,
-                                      double x, double y, double gm, C &gx, C &gy) {
+                                      double x, double y, double gm, C &gx, C &gy, bool last = true) {
     // every slot is evaluated (padded slots hold a copy of planet 0) and the
     // sum selects: a per-planet branch costs more than the arithmetic when
-    // some lane of the wave has all PMAX planets anyway
+    // some lane of the wave has all PMAX planets anyway.  `last` (wave-
+    // uniform) false says no lane has PMAX planets: the last slot is skipped
     C ax = C(0), ay = C(0);
 #pragma unroll
     for (int j = 0; j < PMAX; ++j) {
+        if (j == PMAX - 1 && j > 0 && !last) break;
         const C rx = C(px[j]) - C(x);
         const C ry = C(py[j]) - C(y);
         const C d2 = rx * rx + ry * ry;
@@ -1519,6 +1521,10 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const int flags = (h.y >> 8) & 0xff;
     const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
     np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+    // does any env of the wave use the last planet slot?  (uniform; with
+    // planets_only < PMAX, e.g. the 3-planet games of config 3, none does
+    // and the float64 fields skip that slot's division)
+    const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
     const bool live = tick < p.timeout_tick;
     const bool t0 = tick == 0;
     STAMP(1);
@@ -1590,7 +1596,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             gx = px[0] - mx;
             gy = py[0] - my;
 #else
-            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy);
+            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
 #endif
         }
         const double thr = p.thrust * double(ctl & 1);
@@ -1933,14 +1939,18 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             double Fr[PPL][PMAX];
             if constexpr (LPE == 2 && PMAX == 4) {
                 const bool l0 = q == 0;
-                auto fac = [&](int i, int j) {
-                    const double ddx = px[j] - px[i], ddy = py[j] - py[i];
+                // F(i, j) on lane 0, F(i1, j1) on lane 1: operands selected
+                // first, one division per lane
+                auto fac = [&](int i, int j, int i1, int j1) {
+                    const double ddx = (l0 ? px[j] : px[j1]) - (l0 ? px[i] : px[i1]);
+                    const double ddy = (l0 ? py[j] : py[j1]) - (l0 ? py[i] : py[i1]);
                     return div_gravity(p.gm, max_floor(ddx * ddx + ddy * ddy));
                 };
                 // lane 0: A = F01, B = F03, C = F02; lane 1: A = F12, B = F23, C = F13
-                const double A = l0 ? fac(0, 1) : fac(1, 2);
-                const double B = l0 ? fac(0, 3) : fac(2, 3);
-                const double C = l0 ? fac(0, 2) : fac(1, 3);
+                // (B is only read for planet slot 3: skipped when no env has it)
+                const double A = fac(0, 1, 1, 2);
+                const double B = slot_last ? fac(0, 3, 2, 3) : 0.0;
+                const double C = fac(0, 2, 1, 3);
                 const double A2 = pair_swap(A), B2 = pair_swap(B);   // lane 0: F12, F23; lane 1: F01, F03
                 const double z = 0.0;   // (self: unused)
                 // planet q:     lane 0 [-, F01, F02, F03]   lane 1 [F10, -, F12, F13]
