@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 9
+ABI_VERSION = 11
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
@@ -56,6 +56,7 @@ class AstroState(ctypes.Structure):
         ('bullets', ctypes.c_void_p),
         ('hdr', ctypes.c_void_p),
         ('stream', ctypes.c_void_p),
+        ('stream_ring', ctypes.c_void_p),
         ('n_env', ctypes.c_int32),
         ('state_f64', ctypes.c_int32),
     ]

@@ -42,8 +42,11 @@ def _env(config, bullets_needed):
 
 def create(config):
     """Create a new game state from ``config.seed`` (core.create)."""
+    seed = int(config.seed)
+    if not 0 <= seed < 1 << 32:   # as np.random.RandomState(seed) (core.py:89) refuses it
+        raise ValueError('Seed must be between 0 and 2**32 - 1')
     env = _env(config, 0)
-    env.reset(seeds=[int(config.seed) & 0xFFFFFFFF])
+    env.reset(seeds=[seed])
     return env.state_of(0)
 
 

@@ -1,13 +1,22 @@
 // astro_kernels.hip -- MI355X (gfx950) batched lockstep Astro physics.
 //
-// One lane owns one game ("env"): a wave64 advances 64 independent games.
-// State is struct-of-arrays, entity-major ([slot][env]), so a wave's load of
-// slot s of its 64 envs is one contiguous 1 KiB (float) / 2 KiB (double)
-// stretch -- fully coalesced dwordx4 traffic, the only thing that matters for
-// an HBM-bound kernel.  No LDS: nothing is shared between envs, and each
-// lane's planets live in its own registers (there is no reuse across lanes
-// for LDS to capture).
-//
+// State is struct-of-arrays, entity-major ([slot][env]) for ships and planets
+// (a wave's load of slot s of its envs is one contiguous, coalesced dwordx4
+// stretch) and one contiguous row per env for bullets.  One step kernel in
+// three lane layouts, identical results:
+//   * astro_step_kernel            -- one lane per env (64 envs per wave);
+//                                     registers only, no LDS;
+//   * astro_step_quad_kernel<.., 4> -- four lanes per env (16 envs per wave),
+//   * astro_step_quad_kernel<.., 2> -- two lanes per env (32 envs per wave):
+//     ships and planets move inside an env's lanes by DPP broadcasts; the
+//     wave's live bullets are numbered densely (DPP scan) and indexed through
+//     LDS, one bullet per lane per round; the env's bodies for the bullet
+//     pass and the auto-reset's MT19937 init chains are staged in LDS (one
+//     private LDS set per wave, wave-scoped sync only).
+// Auto-reset runs inside the step (the finished envs' next games, created
+// wave-cooperatively); each env's generate_configs stream is an exact
+// MT19937 of any length (MTStream: cursor + the env's 624-word ring).
+
 // What is computed is exactly astro/core.py's step (core.py:215-303) and
 // create (core.py:86-135), including the reference's numpy dtype behaviour:
 //   * the first step of a game (tick 0) sees create()'s float32 arrays, so
@@ -355,6 +364,46 @@ struct MTLazy {
     }
 };
 
+// An env's generate_configs stream (core.py:77-83) is ONE RandomState drawn
+// for as long as the env plays, so past output 226 the lazy form above no
+// longer holds: output k of MT19937 is
+//     x_{k+624} = x_{k+397} ^ twist(x_k, x_{k+1})      (x_0..x_623 = init key)
+// and from k = 227 on x_{k+397} is an output the generator already made.
+// MTStream keeps the cursor (x_k, x_{k+397}, k) and the env's last 624 twisted
+// words in a ring (ring[j % 624] = x_{j+624}, written by draw j): words
+// 0..226 come from the init chain as in MTLazy, later ones from the ring --
+// the standard one-word-at-a-time MT19937, exact for any length.  A draw's
+// ring loads depend on k only, never on the word being made, so they are
+// issued first.  Draws are rare (one per game, plus planets_only rejections)
+// and the ring is 2.5 KB per env, written one word per draw.
+constexpr uint32_t MT_N = 624;
+constexpr uint32_t MT_LAZY = MT_N - MT_PROLOGUE;   // 227: outputs with x_{k+397} still in the init key
+
+struct MTStream {
+    uint32_t a;      // x_k
+    uint32_t b;      // x_{k+397}
+    uint32_t k;
+    uint32_t *ring;  // the env's [624] words
+
+    __device__ uint32_t next() {
+        const uint32_t k1 = k + 1u;
+        const uint32_t r1 = k1 >= MT_N ? ring[k1 % MT_N] : 0u;                // x_{k+1} = x_{(k+1-624)+624}
+        const uint32_t rb = k1 >= MT_LAZY ? ring[(k1 - MT_LAZY) % MT_N] : 0u;  // x_{k+398}, made by draw k-226
+        const uint32_t x1 = k1 < MT_N ? mt_key_next(a, k1) : r1;
+        const uint32_t y = (a & 0x80000000u) | (x1 & 0x7fffffffu);
+        const uint32_t z = b ^ (y >> 1) ^ ((x1 & 1u) ? 0x9908b0dfu : 0u);
+        ring[k % MT_N] = z;
+        b = k1 < MT_LAZY ? mt_key_next(b, k1 + MT_PROLOGUE) : rb;
+        a = x1;
+        k = k1;
+        return mt_temper(z);
+    }
+};
+
+__device__ __forceinline__ uint32_t *stream_ring_of(const AstroState &st, int i) {
+    return st.stream_ring + size_t(i) * MT_N;
+}
+
 // key[397] of RandomState(seed)'s init chain: one gather from the device
 // table (every 30-bit seed, built once by astro_keytable_build) or, without
 // a table / for a wider explicit seed, the chain itself.
@@ -566,10 +615,10 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, con
 
 // Env i's generate_configs stream (core.py:77-83): RandomState(stream_seed)
 // .randint(1 << 30) = one masked MT word per game.  The stream record holds
-// the cursor (key[k], key[k+397], k) and the CURRENT game's seed; the next
-// game's seed is drawn one game ahead and lives in hdr (.w) with its
-// partially advanced init chain (.z, progress in .x >> 22), so a reset can
-// start creating before the cold stream record arrives.
+// the MTStream cursor (x_k, x_{k+397}, k; the ring beside it) and the CURRENT
+// game's seed; the next game's seed is drawn one game ahead and lives in hdr
+// (.z) with key[397] of its init chain (.w, valid with KEY_VALID), so a
+// reset can start creating before the cold stream record arrives.
 
 // Start env i's next game: its seed was drawn one game ahead (hdr word 2) and
 // key[397] of that seed fetched from the key table by an earlier step (hdr
@@ -584,33 +633,30 @@ struct NextGame {
     CreateWords<S> words;
     uint32_t ca, cb, ci;   // advanced cursor
     uint32_t next_seed;    // the game after
-    bool exhausted;
+    bool exhausted;        // create() ran past the 227 words MTLazy covers
 };
 
 // (key397 of the pending seed is either known or, have_key false, run here)
 template <int S>
 __device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t pend_seed, uint32_t key397,
-                                                 bool have_key, uint32_t ca, uint32_t cb, uint32_t ci) {
+                                                 bool have_key, const uint4 &c, uint32_t *ring) {
     NextGame<S> ng;
-    MTLazy g;
-    g.a = ca;
-    g.b = cb;
-    g.i = ci;
+    MTStream g{c.x, c.y, c.z, ring};
     if (!have_key) key397 = mt_key_at(pend_seed, 0, MT_PROLOGUE);
     // planets_only: the pending seed may not have been checked yet (a game
     // shorter than the steps that check one candidate each): walk the
     // stream here, synchronously
-    while (!seed_passes(p, pend_seed, key397) && g.ok()) {
+    while (!seed_passes(p, pend_seed, key397)) {
         pend_seed = g.next() & SEED_MASK;
         key397 = key397_of(p, pend_seed);
     }
     ng.seed = pend_seed;
     ng.words = create_words<S>(p, pend_seed, key397);
-    ng.exhausted = !g.ok() || ng.words.exhausted;
+    ng.exhausted = ng.words.exhausted;
     ng.next_seed = g.next() & SEED_MASK;
     ng.ca = g.a;
     ng.cb = g.b;
-    ng.ci = g.i;
+    ng.ci = g.k;
     return ng;
 }
 
@@ -639,14 +685,10 @@ __device__ __forceinline__ uint32_t check_pending(const AstroParams &p, const As
     if (key_valid) return KEY_VALID;
     if (!p.key_table) return 0u;
     if (seed_passes(p, seed, key)) return KEY_VALID;
-    MTLazy g;
-    g.a = c.x;
-    g.b = c.y;
-    g.i = c.z;
-    if (!g.ok()) return KEY_VALID;   // stream exhausted (flagged at the game's create): keep it
+    MTStream g{c.x, c.y, c.z, stream_ring_of(st, i)};
     seed = g.next() & SEED_MASK;
     key = 0u;
-    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, c.w);
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.k, c.w);
     return 0u;
 }
 
@@ -1093,7 +1135,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             f_tout = timeout;
             if (auto_reset) {
                 const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-                const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, c.x, c.y, c.z);
+                const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, c, stream_ring_of(st, i));
                 restart_env<T, S, PMAX>(p, st, i, ng);
                 f_reset = true;
             }
@@ -1426,14 +1468,10 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     }
     if (on && fast) {
         if (u == 0) {   // the stream record and header, as restart_env
-            MTLazy g;
-            g.a = c.x;
-            g.b = c.y;
-            g.i = c.z;
-            const bool exhausted = !g.ok();
+            MTStream g{c.x, c.y, c.z, stream_ring_of(st, ie)};
             const uint32_t next_seed = g.next() & SEED_MASK;
-            reinterpret_cast<uint4 *>(st.stream)[ie] = make_uint4(g.a, g.b, g.i, seed);
-            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | ((exhausted || cf) ? 2 << 8 : 0), int(next_seed), 0);
+            reinterpret_cast<uint4 *>(st.stream)[ie] = make_uint4(g.a, g.b, g.k, seed);
+            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | (cf ? 2 << 8 : 0), int(next_seed), 0);
         }
     }
     if (on && !fast && u == 0) s_serial[L / LPE] = 1;
@@ -2061,7 +2099,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         if (active && s_serial[e]) {   // uniform over the quad; rare
             const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(pend_key)));   // lane q == 0 fetched it
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
-            const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, c.x, c.y, c.z);
+            const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, c, stream_ring_of(st, is));
             restart_env<T, S, PMAX, LPE>(p, st, is, ng, q);
         }
     }
@@ -2086,8 +2124,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 }
 
 // Add one tick's counters to the wave's private stats row (lane 0).  A
-// lane's per-tick counts are < 2^16 and, for b_cap < 4,096, so are their
-// sums over the wave's 16 envs: two counters then share one wave sum.
+// lane's per-tick counts are < 2^16 and, for b_cap * (envs per wave) <
+// 65,536, so are their sums over the wave's envs: two counters then share
+// one wave sum.
 __device__ __forceinline__ void flush_counts(unsigned long long *slot, const QuadCounts &c, bool packed) {
     const uint32_t a = wave_sum32(packed ? (c.n_bin | (c.n_bout << 16)) : c.n_bin);
     const uint32_t b = wave_sum32(packed ? (c.n_pl | (c.n_drop << 16)) : c.n_bout);
@@ -2159,7 +2198,7 @@ __global__ __launch_bounds__(QBLOCK, MULTI ? 2 : 4) void astro_step_quad_kernel(
         }
         if (stats)
             flush_counts(stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * ASTRO_NSTATS, c,
-                         p.b_cap < 4096);
+                         p.b_cap * (64 / LPE) < 65536);
         // this tick's stores (other lanes' bullets included) before the
         // wave's next tick reads them: vmcnt(0), on this CU's own L1
         if (kt + 1 < n_ticks) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -2285,7 +2324,7 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
         const uint32_t seed = uint32_t(h.z);
         const uint32_t key = (uint32_t(h.x) & KEY_VALID) ? uint32_t(h.w) : key397_of(p, seed);
         const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, c.x, c.y, c.z));
+        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, c, stream_ring_of(st, i)));
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued
@@ -2301,10 +2340,10 @@ __global__ __launch_bounds__(BLOCK) void astro_stream_init_kernel(AstroState st,
                                                                   const uint32_t *__restrict__ seeds) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= st.n_env) return;
-    MTLazy g;
-    g.seed(seeds[i]);
-    const uint32_t first = g.next() & ((1u << 30) - 1);   // game 0's seed, pending
-    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.i, 0u);
+    const uint32_t s0 = seeds[i];
+    MTStream g{s0, mt_key_at(s0, 0, MT_PROLOGUE), 0u, stream_ring_of(st, i)};
+    const uint32_t first = g.next() & SEED_MASK;   // game 0's seed, pending
+    reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(g.a, g.b, g.k, 0u);
     reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, 1, int(first), 0);
 }
 
@@ -2355,6 +2394,9 @@ int check_state(const AstroState *s) {
         return fail(-5, "ships/planets/bullets must be 16-byte aligned");
     if ((reinterpret_cast<uintptr_t>(s->hdr) & 15u) != 0) return fail(-5, "hdr must be 16-byte aligned");
     if (s->state_f64 != 0 && s->state_f64 != 1) return fail(-6, "state_f64 must be 0 or 1");
+    if (s->stream && !aligned16(s->stream)) return fail(-5, "stream must be 16-byte aligned");
+    if (s->stream && (!s->stream_ring || (reinterpret_cast<uintptr_t>(s->stream_ring) & 3u)))
+        return fail(-7, "the stream array needs its stream_ring ([n_env][624] uint32, 4-byte aligned)");
     return 0;
 }
 
@@ -2561,6 +2603,8 @@ int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *s
     if (s->n_env == 0) return 0;
     if (!s->stream || !stream_seeds) return fail(-41, "stream / stream_seeds is NULL");
     if (reinterpret_cast<uintptr_t>(s->stream) & 15u) return fail(-5, "stream must be 16-byte aligned");
+    if (!s->stream_ring || (reinterpret_cast<uintptr_t>(s->stream_ring) & 3u))
+        return fail(-7, "the stream array needs its stream_ring ([n_env][624] uint32, 4-byte aligned)");
     if (!s->hdr || (reinterpret_cast<uintptr_t>(s->hdr) & 15u)) return fail(-5, "hdr must be 16-byte aligned");
     const int grid = (s->n_env + BLOCK - 1) / BLOCK;
     hipLaunchKernelGGL(astro_stream_init_kernel, dim3(grid), dim3(BLOCK), 0,

@@ -19,6 +19,7 @@ per env (the kernels walk an env's live bullets in slot order):
     hdr      [N, 4]      tick | chain << 22, nplanets | flags << 8 | nbullets << 16,
                          next game's init-chain value, next game's seed
     stream   [N, 4]      seed-stream cursor + current game's seed
+    stream_ring [N, 624] the stream's MT19937 state words (exact for any length)
 
 and every call goes through libastro_hip.so (include/astro_step.h) on the
 current torch stream.  There is no CPU path.
@@ -35,6 +36,7 @@ from .config import Bodies, State, nships as _nships
 from . import schedule as _schedule
 
 TICK_MASK = (1 << 22) - 1
+MT_N = 624   # MT19937 state words: each env's seed stream keeps its own (stream_ring)
 
 Observation = collections.namedtuple(
     'Observation', ('ships', 'ships_b', 'planets', 'nplanets', 'bullets', 'nbullets', 'tick'))
@@ -122,6 +124,7 @@ class BatchedEnv:
         self.bullets = z(N, self.b_cap, 4)
         self.hdr = z(N, 4, dt=torch.int32)
         self.stream = z(N, 4, dt=torch.int32)
+        self.stream_ring = z(N, MT_N, dt=torch.int32)
         self.reward = z(N, S, dt=torch.float32)
         self.done = z(N, dt=torch.uint8)
         self.stats = z(max(1, (N + 15) // 16), _lib.NSTATS, dt=torch.int64)
@@ -137,6 +140,7 @@ class BatchedEnv:
             ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),
             planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),
             hdr=self.hdr.data_ptr(), stream=self.stream.data_ptr(),
+            stream_ring=self.stream_ring.data_ptr(),
             n_env=N, state_f64=1 if dtype == torch.float64 else 0)
 
         self.stream_seeds = _shard.stream_seeds(config, self.env_offset, N)
@@ -319,7 +323,7 @@ class BatchedEnv:
         old = self.hdr.cpu().numpy().view(np.uint32).astype(np.int64)
         hdr = old.copy()
         hdr[:, 0] = (old[:, 0] & ~TICK_MASK & 0xFFFFFFFF) | np.asarray(tick, np.int64)
-        hdr[:, 1] = np.asarray(nplanets, np.int64) | (nb << 16)
+        hdr[:, 1] = np.asarray(nplanets, np.int64) | (old[:, 1] & 0xff00) | (nb << 16)
         self.hdr.copy_(torch.as_tensor(hdr.astype(np.uint32).view(np.int32)).to(dev))
 
     def state_of(self, i, host=None):

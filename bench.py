@@ -88,16 +88,29 @@ def cpu_baseline(cfg_kw, seconds, procs, planets_only=0):
                 per_core=steps / wall / procs)
 
 
+def cpu_share():
+    """Host cores this process may use: OMP_NUM_THREADS when the launcher
+    set it (the GPU box's per-GPU CPU share), else the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        omp = int(os.environ.get('OMP_NUM_THREADS', '0'))
+    except ValueError:
+        omp = 0
+    return max(1, min(n, omp) if omp > 0 else n)
+
+
 def algorithmic_bytes(env, dstats, launches):
-    """Bytes a launch must move: per env header r/w (16), ships r/w
-    (2*S*5 elems), control S, reward 4S, done 1; per live planet r/w (8 elems);
-    per live bullet read or written (4 elems); per reset the seed-stream
-    cursor r/w (32)."""
+    """SURVEY.md section 8(d)'s bytes per env-step, summed over a launch:
+    2 * (20 S + 16 P + 16 B + 12) + S + 4 S + 1 -- header (3 words), ships
+    (x, y, dx, dy, b), live planets and live bullets read and written, int8
+    control in, float32 reward and uint8 done out -- with P and B the live
+    planets and bullets the kernel's own counters saw (a bullet read,
+    bullets_in, or written, bullets_out, counts once; 8-byte elements for
+    float64 state)."""
     e = 8 if env.dtype == torch.float64 else 4
     S, N = env.S, env.n_env
-    fixed = launches * N * (16 + 2 * S * 5 * e + S + 4 * S + 1)
-    var = (8 * e * dstats['planets'] + 4 * e * (dstats['bullets_in'] + dstats['bullets_out'])
-           + 32 * dstats['resets'])
+    fixed = launches * N * (2 * (5 * e * S + 12) + S + 4 * S + 1)
+    var = 2 * 4 * e * dstats['planets'] + 4 * e * (dstats['bullets_in'] + dstats['bullets_out'])
     return (fixed + var) / launches
 
 
@@ -110,7 +123,13 @@ def main():
     ap.add_argument('--n-env', type=int, default=0, help='override envs per GPU')
     ap.add_argument('--state', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
-    ap.add_argument('--cpu-procs', type=int, default=1)
+    ap.add_argument('--cpu-procs', type=int, default=0,
+                    help='host processes for the CPU baseline (0 = one per core of the '
+                         "process's CPU share: OMP_NUM_THREADS if set, else its affinity mask)")
+    ap.add_argument('--burn-in', type=int, default=300,
+                    help='ticks every env plays (one astro_rollout launch, on-device random '
+                         'controls) before the warmup, so the timed region sees steady-state '
+                         'games (live bullets, resets) whatever --warmup is')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--traffic', default='', help='JSON with PMC-measured HBM bytes per launch')
     ap.add_argument('--kernel', default='auto', choices=['auto', 'lane', 'quad', 'pair'])
@@ -150,6 +169,8 @@ def main():
                      dtype=torch.float64 if args.state == 'f64' else torch.float32,
                      env_offset=offset, auto_reset=True, kernel=args.kernel, planets_only=wl['planets_only'])
     env.reset()
+    if args.burn_in > 0:   # age the batch: games of every age, bullets in flight
+        env.rollout(args.burn_in, 'random', tick0=1 << 40, stats=False)
     ticks = args.warmup + args.steps
     ctl = torch.from_numpy(controls(offset, n, env.S, ticks)).to(dev)
     ptrs = [ctl[t].data_ptr() for t in range(ticks)]
@@ -255,8 +276,12 @@ def main():
 
     wall_max = _shard.max_over_ranks(wall, device=red_dev)
     d = {k: s1[k] - s0[k] for k in s0}
+    fl = env.flags
     tot = _shard.sum_over_ranks([d[k] for k in ('bullets_in', 'resets', 'overflows', 'collisions',
-                                                'timeouts')], device=red_dev)
+                                                'timeouts')]
+                                + [int(((fl & 1) != 0).sum()), int(((fl & 2) != 0).sum())], device=red_dev)
+    # distinct devices behind the ranks (a one-GPU rehearsal shares one)
+    n_dev = int(_shard.sum_over_ranks([1 if local < torch.cuda.device_count() else 0], device=red_dev)[0])
     bytes_launch = algorithmic_bytes(env, d, args.steps)
 
     if rank == 0:
@@ -267,23 +292,34 @@ def main():
         # (profiles/round1); one event pair per eager launch adds ~2.5 us
         launch_ms = gpu_ms_per_step
         achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
+        # PMC-measured HBM bytes and VALU instructions per launch come from
+        # committed rocprofv3 runs of this same command (profiles/round2/);
+        # they are used only when that run saw the same workload state
+        # (envs, kernel, mean live bullets and resets per launch within 10%)
+        mlb = tot[0] / (n_total * args.steps)
+        rps = tot[1] / args.steps
+
+        def matching(path):
+            if not os.path.exists(path):
+                return None
+            with open(path) as f:
+                j = json.load(f)
+            ok = (j.get('n_env') == n and j.get('kernel') in (args.kernel, 'auto', env.step_kernel)
+                  and abs(j.get('mean_live_bullets', -1) - mlb) <= 0.1 * max(mlb, 0.05) + 1e-9
+                  and abs(j.get('resets_per_step', -1) - rps) <= 0.1 * max(rps, 1.0))
+            return j if ok else None
         traffic = None
-        tpath = args.traffic or os.path.join(ROOT, 'profiles', 'round1', 'traffic_%s_%s.json' % (
-            args.workload, args.state))
-        if os.path.exists(tpath):
-            with open(tpath) as f:
-                tj = json.load(f)
-            if tj.get('n_env') == n and tj.get('kernel') in (args.kernel, 'auto'):
-                traffic = tj.get('hbm_bytes_per_launch')
+        tj = matching(args.traffic or os.path.join(ROOT, 'profiles', 'round2', 'traffic_%s_%s.json' % (
+            args.workload, args.state)))
+        if tj:
+            traffic = tj.get('hbm_bytes_per_launch')
         # secondary bound: VALU issue, from the committed PMC instruction count
-        # of this workload's kernel (profiles/round1/pmc_<workload>_<state>.json)
+        # of this workload's kernel (profiles/round2/pmc_<workload>_<state>.json)
         issue = None
-        ppath = os.path.join(ROOT, 'profiles', 'round1', 'pmc_%s_%s.json' % (args.workload, args.state))
-        if os.path.exists(ppath):
-            with open(ppath) as f:
-                pj = json.load(f)
+        pj = matching(os.path.join(ROOT, 'profiles', 'round2', 'pmc_%s_%s.json' % (args.workload, args.state)))
+        if pj:
             lpe = dict(lane=1, quad=4, pair=2)[env.step_kernel]
-            if pj.get('n_env') == n and pj.get('lanes_per_env') == lpe:
+            if pj.get('lanes_per_env') == lpe:
                 rate = pj['waves'] * pj['valu_per_wave'] / (launch_ms * 1e-3)
                 peak = 256 * 4 * 2.4e9 / 4
                 issue = dict(bound='valu-issue', achieved=rate, peak=peak, unit='wave-instructions/s',
@@ -291,7 +327,7 @@ def main():
                              note='not HBM-bound and not issue-bound: two waves per SIMD at c3, '
                                   'latency-bound (DESIGN.md section 3)')
         out = dict(
-            metric=METRIC, value=value, unit='env-steps/s', n_gpus=world, steps=args.steps,
+            metric=METRIC, value=value, unit='env-steps/s', n_gpus=n_dev, ranks=world, steps=args.steps,
             warmup=args.warmup, ms_per_step=wall_max / args.steps * 1e3, higher_is_better=True,
             scaling='weak', vs_baseline=None,
             dtype='f64' if args.state == 'f64' else 'f64 math / f32 state',
@@ -308,17 +344,21 @@ def main():
                           timing='hipEvent pair around the timed region / K launches'),
             issue_roofline=issue,
             gpu_ms_per_step=gpu_ms_per_step,
-            timed_region='%d launches, %s' % (args.steps, 'hipGraph replays of %d launches' % args.graph
-                                              if args.graph else 'eager'),
-            stats=dict(mean_live_bullets=tot[0] / (n_total * args.steps),
+            timed_region='%d launches, %s' % (
+                args.steps, ('replayed as %d hipGraph(s) of up to %d launches' % (len(graphs), args.graph))
+                if graphs else 'launched eagerly'),
+            burn_in_ticks=args.burn_in,
+            stats=dict(mean_live_bullets=mlb,
                        serial_resets_per_step=d.get('serial_resets', 0) / args.steps,
-                       resets_per_step=tot[1] / args.steps, overflow_bullets=tot[2],
+                       resets_per_step=rps, overflow_bullets=tot[2],
                        collisions=tot[3], timeouts=tot[4],
-                       mean_planets=d['planets'] / (n * args.steps)),
+                       mean_planets=d['planets'] / (n * args.steps),
+                       envs_flag_overflow=tot[5], envs_flag_create_exhausted=tot[6]),
         )
         out.update(extras)
         if world == 1 and not args.no_cpu:
-            out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, args.cpu_procs, wl['planets_only'])
+            procs = args.cpu_procs or cpu_share()
+            out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, procs, wl['planets_only'])
             out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']
         print(json.dumps(out), flush=True)
     if world > 1:

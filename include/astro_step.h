@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 9
+#define ASTRO_ABI_VERSION 11
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -93,7 +93,8 @@ enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2, ASTR
  *   hdr[4*i+2] = the NEXT game's seed (drawn one game ahead from the stream)
  *   hdr[4*i+3] = key[397] of that seed's MT19937 init chain (when key_valid)
  * flags: bit0 = a bullet was dropped (b_cap full) this game,
- *        bit1 = the env's seed stream ran past its 227 exact games.
+ *        bit1 = create() needed more than 227 words of its seed's MT19937
+ *               (masked randint rejections; unreachable in practice).
  * A running step fetches the next game's key[397] from the key table once,
  * so an auto-reset never runs the 397-step chain inline. */
 typedef struct AstroState {
@@ -102,7 +103,11 @@ typedef struct AstroState {
     void *planets;      /* [p_pad][n_env][4]   x, y, dx, dy */
     void *bullets;      /* [n_env][b_cap][4]   x, y, dx, dy (one contiguous row per env) */
     int32_t *hdr;       /* [n_env][4], 16-byte aligned */
-    uint32_t *stream;   /* [n_env][4] generate_configs cursor: key[k], key[k+397], k, current game's seed */
+    uint32_t *stream;   /* [n_env][4] generate_configs cursor: x_k, x_{k+397}, k, current game's seed
+                           (x = the MT19937 word sequence of the env's RandomState, core.py:79) */
+    uint32_t *stream_ring; /* [n_env][624] the env's last 624 twisted MT19937 words (MT's own state,
+                              kept one word per draw): required with `stream`; the library
+                              writes it before it reads it, no initialisation needed */
     int32_t n_env;
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
 } AstroState;

@@ -380,7 +380,7 @@ def filtered_game_seeds(env_stream_seeds, n_games, planets, max_planets, draws=2
     max_planets + 1) (core.py:90) is the first word of RandomState(seed)
     masked, max_planets a power of two."""
     cand = game_seeds(env_stream_seeds, draws)                       # [N, draws]
-    first = mt19937.words(cand.reshape(-1), 1).reshape(cand.shape)
+    first = mt19937.first_words(cand).reshape(cand.shape)
     n = 1 + (first & np.uint32(max_planets - 1)).astype(np.int64)
     out = np.zeros((len(env_stream_seeds), n_games), np.uint32)
     for i in range(len(env_stream_seeds)):
@@ -388,6 +388,23 @@ def filtered_game_seeds(env_stream_seeds, n_games, planets, max_planets, draws=2
         assert len(ok) >= n_games, 'increase draws'
         out[i] = ok[:n_games]
     return out
+
+
+def filtered_game_draws(env_stream_seeds, n_games, planets, max_planets, draws):
+    """Like filtered_game_seeds, plus the stream index (0-based draw number
+    of RandomState(stream_seed)) each game's seed came from: [N, n_games]
+    seeds, [N, n_games] draw indices."""
+    cand = game_seeds(env_stream_seeds, draws)
+    first = mt19937.first_words(cand).reshape(cand.shape)
+    n = 1 + (first & np.uint32(max_planets - 1)).astype(np.int64)
+    seeds = np.zeros((len(env_stream_seeds), n_games), np.uint32)
+    idx = np.zeros((len(env_stream_seeds), n_games), np.int64)
+    for i in range(len(env_stream_seeds)):
+        k = np.nonzero(n[i] == planets)[0]
+        assert len(k) >= n_games, 'increase draws'
+        idx[i] = k[:n_games]
+        seeds[i] = cand[i][idx[i]]
+    return seeds, idx
 
 
 def collisions_allpairs(x, r):

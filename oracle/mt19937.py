@@ -71,6 +71,19 @@ def words(seeds, count):
     return np.concatenate(out, axis=1)[:, :count].astype(np.uint32)
 
 
+def first_words(seeds):
+    """Output 0 of RandomState(seed) for each seed -> [K] uint32: it needs
+    only init-key words 0, 1 and 397 (the 397-step chain, no 624-word state)."""
+    s = np.asarray(seeds, dtype=np.uint64).reshape(-1) & MASK32
+    k1 = (np.uint64(1812433253) * (s ^ (s >> np.uint64(30))) + np.uint64(1)) & MASK32
+    v = k1.copy()
+    for i in range(2, M + 1):
+        v = (np.uint64(1812433253) * (v ^ (v >> np.uint64(30))) + np.uint64(i)) & MASK32
+    y = (s & UPPER) | (k1 & LOWER)
+    mag = np.where((y & np.uint64(1)) != 0, MATRIX_A, np.uint64(0))
+    return temper(v ^ (y >> np.uint64(1)) ^ mag).astype(np.uint32)
+
+
 class Stream:
     """A cursor over one seed's raw words with the legacy draw rules."""
 

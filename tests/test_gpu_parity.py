@@ -127,6 +127,39 @@ def test_planets_only_streams(kernel, fast_end):
     assert games.max() > 2
 
 
+@pytest.mark.parametrize('kernel', KERNELS)
+def test_config2_exact_vs_oracle(kernel):
+    """BASELINE.json config 2 as bench.py runs it: 4,096 envs,
+    DEFAULT_CONFIG with reload_time=1000 (no bullets), 2 ships, games
+    filtered to 3 planets, auto-reset -- 200 ticks, every tick equal to the
+    oracle stepped from the kernel's own float32 input state, every new game
+    the oracle's create() of the stream's next 3-planet seed."""
+    cfg = CFG['default']._replace(reload_time=1000)
+    P = batched.make_params(cfg)
+    n, ticks = 4096, 200
+    from astro_amd import BatchedEnv
+    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=32, p_pad=4, planets_only=3, kernel=kernel)
+    env.reset()
+    seeds = batched.filtered_game_seeds(env.stream_seeds, 16, 3, cfg.max_planets, draws=220)
+    games = np.ones(n, np.int64)
+    rng = np.random.RandomState(22)
+    for t in range(ticks):
+        B = _host_batch(env)
+        assert (B.nplanets == 3).all() and (B.nbullets == 0).all(), t
+        ctl = rng.randint(0, 6, size=(n, 2)).astype(np.int8)
+        want, wrew, wdone = batched.step(B, ctl, P, store='f32')
+        fin = np.nonzero(wdone)[0]
+        if fin.size:
+            want.put(fin, batched.create(seeds[fin, games[fin]], P, p_pad=env.p_pad, b_cap=32, store='f32'))
+            games[fin] += 1
+        _, rew, done = env.step(torch.from_numpy(ctl).cuda())
+        assert (done.cpu().numpy() == wdone).all(), t
+        assert np.array_equal(rew.cpu().numpy(), wrew), t
+        _assert_same('c2 t=%d' % t, _host_batch(env), want, np.ones(n, bool), rounding=True)
+    st = env.stat_dict()
+    assert st['bullets_in'] == 0 and st['resets'] == int((games - 1).sum()) > 0
+
+
 # ------------------------------------------------- teacher-forced transitions
 
 @pytest.mark.parametrize('kernel', KERNELS)
@@ -316,6 +349,37 @@ def test_full_size_determinism_and_shard_invariance():
     assert int(nb.max()) <= 32 and int(a.nplanets.min()) >= 1 and int(a.nplanets.max()) <= 4
     st = a.stat_dict()
     assert st['resets'] == st['collisions'] + st['timeouts'] > 0
+
+
+def test_config4_eight_shards_compose():
+    """BASELINE.json config 4's sharding on one GPU: 8 BatchedEnv shards of
+    65,536 envs (env_offset = rank * 65,536, as bench.py's ranks) stepped
+    200 ticks equal one 524,288-env run bit for bit -- headers, stream
+    cursors and rings, ships, planets, bullets."""
+    cfg = CFG['default']
+    n, G, ticks = 65536, 8, 200
+    from astro_amd import BatchedEnv
+    g = torch.Generator(device='cuda').manual_seed(4)
+    ctls = torch.randint(0, 6, (ticks, n * G, 2), generator=g, device='cuda', dtype=torch.int8)
+    full = BatchedEnv(cfg, n * G, device='cuda:0', b_cap=32, p_pad=4, planets_only=3)
+    full.reset()
+    for t in range(ticks):
+        full.step(ctls[t])
+    for r in range(G):
+        env = BatchedEnv(cfg, n, device='cuda:0', b_cap=32, p_pad=4, planets_only=3, env_offset=r * n)
+        env.reset()
+        for t in range(ticks):
+            env.step(ctls[t, r * n:(r + 1) * n].contiguous())
+        sl = slice(r * n, (r + 1) * n)
+        assert torch.equal(env.hdr, full.hdr[sl]), r
+        assert torch.equal(env.stream, full.stream[sl]), r
+        assert torch.equal(env.stream_ring, full.stream_ring[sl]), r
+        assert torch.equal(env.ships, full.ships[:, sl]), r
+        assert torch.equal(env.ships_b, full.ships_b[:, sl]), r
+        assert torch.equal(env.planets, full.planets[:, sl]), r
+        assert torch.equal(env.bullets, full.bullets[sl]), r
+        del env
+    assert int(full.stat_dict()['resets']) > 0
 
 
 @pytest.mark.parametrize('kernel', KERNELS)

@@ -201,3 +201,58 @@ def test_planets_only_validation():
         BatchedEnv(DEFAULT_CONFIG._replace(max_planets=3), 4, device='cuda:0', planets_only=2)
     with _pytest.raises(ValueError):
         BatchedEnv(DEFAULT_CONFIG, 4, device='cuda:0', planets_only=5)
+
+
+def test_mtstream_ring_algorithm_matches_numpy():
+    """The kernel's MTStream (astro_kernels.hip): cursor (x_k, x_{k+397}, k)
+    + a 624-word ring, one word per draw, restated here line for line --
+    equals numpy's RandomState(seed) for 2,000 outputs (past 227, where the
+    lazy init-key form ends, and past 624 and 1,248, whole twists)."""
+    M32 = 0xFFFFFFFF
+
+    def key_next(prev, idx):
+        return (1812433253 * (prev ^ (prev >> 30)) + idx) & M32
+
+    def temper(y):
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9d2c5680
+        y ^= (y << 15) & 0xefc60000
+        return y ^ (y >> 18)
+
+    for seed in (0, 42, 5489, (1 << 32) - 1):
+        a, b, k = seed, seed, 0
+        for i in range(1, 398):
+            b = key_next(b, i)
+        ring = [None] * 624
+        out = []
+        for _ in range(2000):
+            k1 = k + 1
+            r1 = ring[k1 % 624] if k1 >= 624 else 0
+            rb = ring[(k1 - 227) % 624] if k1 >= 227 else 0
+            x1 = key_next(a, k1) if k1 < 624 else r1
+            y = (a & 0x80000000) | (x1 & 0x7fffffff)
+            z = b ^ (y >> 1) ^ (0x9908b0df if x1 & 1 else 0)
+            ring[k % 624] = z
+            b = key_next(b, k1 + 397) if k1 < 227 else rb
+            a, k = x1, k1
+            out.append(temper(z))
+        ref = np.random.RandomState(seed).randint(0, 1 << 32, size=2000, dtype=np.uint64)
+        assert out == [int(v) for v in ref]
+
+
+def test_first_words_and_long_filtered_streams_match_numpy():
+    """oracle.mt19937.first_words (create()'s planet-count word, core.py:90)
+    and filtered_game_draws over 1,500 stream draws == numpy itself."""
+    import itertools
+    from oracle import mt19937
+    from astro_amd.config import generate_configs_filtered
+    seeds = np.array([0, 1, 42, 5489, 123456789, (1 << 30) - 1, (1 << 32) - 1])
+    ref = [np.random.RandomState(int(s)).randint(0, 1 << 32, dtype=np.uint64) for s in seeds]
+    assert list(mt19937.first_words(seeds)) == [int(r) for r in ref]
+    ss = batched.stream_seeds(7, 3)
+    got, idx = batched.filtered_game_draws(ss, 300, 3, 4, 1500)
+    for i in range(3):
+        want = [c.seed for c in itertools.islice(
+            generate_configs_filtered(DEFAULT_CONFIG._replace(seed=int(ss[i])), 3), 300)]
+        assert list(got[i]) == want
+    assert idx.max() > 1000

@@ -577,7 +577,99 @@ def gen_script_controls():
     print('wrote script_controls.npz', out.shape[0], 'states')
 
 
+# ---------------------------------------------------------------------------
+# 9. BASELINE.json config 1: DEFAULT_CONFIG (seed 42), 1000 ticks of
+#    RandomState(0).randint(0, 6, (1000, 2)) controls, re-created on done
+
+def gen_config1():
+    config = core.DEFAULT_CONFIG
+    ctl = np.random.RandomState(0).randint(0, 6, (1000, 2))
+    state = core.create(config)
+    ships, planets, npl, bl, boff, rew, done, gtick = [], [], [], [], [0], [], [], []
+    g = 0
+    for t in range(1000):
+        sp, pp, n, b, _ = pack_state(state, 2)
+        ships.append(sp)
+        planets.append(pp)
+        npl.append(n)
+        bl.append(b)
+        boff.append(boff[-1] + b.shape[0])
+        gtick.append(g)
+        state, reward = core.step(state, ctl[t], config)
+        rew.append(np.asarray(reward, np.float64))
+        if state is None:
+            done.append(1 if reward.dtype.kind == 'i' else 2)
+            state = core.create(config)
+            g = 0
+        else:
+            done.append(0)
+            g += 1
+    np.savez_compressed(os.path.join(OUT, 'config1.npz'), control=ctl.astype(np.int8),
+                        ships=np.stack(ships), planets=np.stack(planets), nplanets=np.array(npl, np.int32),
+                        bullets=np.concatenate(bl).reshape(-1, 4), bullets_off=np.array(boff, np.int64),
+                        reward=np.stack(rew), done=np.array(done, np.int8), game_tick=np.array(gtick, np.int32))
+    print('wrote config1.npz', int(np.sum(np.array(done) > 0)), 'games ended')
+
+
+# ---------------------------------------------------------------------------
+# 10. Whole games to the end under the reference's own bots (core.play):
+#     test_script's invariants (test/test_core.py:88-98, max_time=20) and
+#     games that reach the full 3000-tick timeout (core.py:257-260)
+
+def _record_play(key, config, bots, out, index, extra):
+    game = core.play(config, bots)
+    nships = 1 if config.solo else 2
+    ctl = np.stack([t.control for t in game.ticks]).astype(np.int8)
+    ships = np.stack([pack_state(t.state, nships)[0] for t in game.ticks])
+    nbul = np.array([t.state.bullets.x.shape[0] for t in game.ticks], np.int32)
+    reward = game.ticks[-1].reward
+    rew = np.zeros(2)
+    rew[:nships] = reward
+    out[key + '__controls'] = ctl
+    out[key + '__ships'] = ships
+    out[key + '__nbullets'] = nbul
+    out[key + '__reward'] = rew
+    index.append(dict(key=key, config=dict(config._asdict()), ticks=len(game.ticks), winner=game.winner,
+                      done=1 if reward.dtype.kind == 'i' else 2, **extra))
+    return game
+
+
+def gen_long_games():
+    out, index = {}, {}
+    rows = []
+    # test_script (test_core.py:88-98)
+    for k, config in enumerate(it.islice(core.generate_configs(core.SOLO_CONFIG._replace(max_time=20)), 3)):
+        _record_play('script_solo%d' % k, config, [script.ScriptBot.create(config)], out, rows,
+                     dict(bots=['script']))
+    for k, config in enumerate(it.islice(core.generate_configs(core.DEFAULT_CONFIG._replace(max_time=20)), 3)):
+        _record_play('nothing_script%d' % k, config, [script.NothingBot(), script.ScriptBot.create(config)],
+                     out, rows, dict(bots=['nothing', 'script']))
+    # a full-length game: the first SOLO game ScriptBot survives to the
+    # 3000-tick timeout (no 1v1 ScriptBot game of the first 40 DEFAULT_CONFIG
+    # configs lasts that long)
+    for name, base, mk in [('solo_timeout', core.SOLO_CONFIG, lambda c: [script.ScriptBot.create(c)])]:
+        for config in it.islice(core.generate_configs(base), 40):
+            game = core.play(config, mk(config))
+            if len(game.ticks) == 3000:
+                _record_play(name, config, mk(config), out, rows,
+                             dict(bots=['script'] * (1 if config.solo else 2)))
+                break
+        else:
+            print('no', name, 'game found')
+    index = rows
+    np.savez_compressed(os.path.join(OUT, 'long_games.npz'), **out)
+    with open(os.path.join(OUT, 'long_games.json'), 'w') as f:
+        json.dump(index, f, indent=0)
+    print('wrote long_games.npz', [(r['key'], r['ticks'], r['winner']) for r in index])
+
+
 def main():
+    if sys.argv[1:] == ['config1']:
+        gen_config1()
+        return
+    if sys.argv[1:] == ['long']:
+        gen_long_games()
+        return
     if sys.argv[1:] == ['script']:
         gen_script_controls()
         return
@@ -600,6 +692,8 @@ def main():
     gen_features()
     gen_log()
     gen_script_controls()
+    gen_config1()
+    gen_long_games()
 
 
 if __name__ == '__main__':
