@@ -386,14 +386,35 @@ struct MTStream {
     uint32_t *ring;  // the env's [624] words
 
     __device__ uint32_t next() {
+#ifdef ASTRO_ABLATE_RING   // timing ablation only: the lazy form (wrong past output 226)
+        {
+            const uint32_t x1 = mt_key_next(a, k + 1u);
+            const uint32_t y = (a & 0x80000000u) | (x1 & 0x7fffffffu);
+            const uint32_t z = b ^ (y >> 1) ^ ((x1 & 1u) ? 0x9908b0dfu : 0u);
+            b = mt_key_next(b, k + 1u + MT_PROLOGUE);
+            a = x1;
+            ++k;
+            return mt_temper(z);
+        }
+#endif
         const uint32_t k1 = k + 1u;
-        const uint32_t r1 = k1 >= MT_N ? ring[k1 % MT_N] : 0u;                // x_{k+1} = x_{(k+1-624)+624}
-        const uint32_t rb = k1 >= MT_LAZY ? ring[(k1 - MT_LAZY) % MT_N] : 0u;  // x_{k+398}, made by draw k-226
-        const uint32_t x1 = k1 < MT_N ? mt_key_next(a, k1) : r1;
+        uint32_t x1, nb;
+        if (k1 < MT_LAZY) {   // x_{k+1} and x_{k+398} still in the init key: no memory
+            x1 = mt_key_next(a, k1);
+            nb = mt_key_next(b, k1 + MT_PROLOGUE);
+        } else {
+            const uint32_t r1 = k1 >= MT_N ? ring[k1 % MT_N] : 0u;   // x_{k+1} = x_{(k+1-624)+624}
+            nb = ring[(k1 - MT_LAZY) % MT_N];                        // x_{k+398}, made by draw k-226
+            x1 = k1 < MT_N ? mt_key_next(a, k1) : r1;
+            // consume the loads here: a use after the join would put the
+            // wait for them (vmcnt, which also counts every store and
+            // prefetch in flight) on the lazy path too
+            asm volatile("" ::"v"(x1), "v"(nb));
+        }
         const uint32_t y = (a & 0x80000000u) | (x1 & 0x7fffffffu);
         const uint32_t z = b ^ (y >> 1) ^ ((x1 & 1u) ? 0x9908b0dfu : 0u);
         ring[k % MT_N] = z;
-        b = k1 < MT_LAZY ? mt_key_next(b, k1 + MT_PROLOGUE) : rb;
+        b = nb;
         a = x1;
         k = k1;
         return mt_temper(z);
@@ -2164,7 +2185,10 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 
 template <typename T, int S, int PMAX, bool MULTI, int LPE>
-__global__ __launch_bounds__(QBLOCK, MULTI ? 2 : 4) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+#ifndef ASTRO_P8_WAVES
+#define ASTRO_P8_WAVES 3   // 8 planet slots: 141 VGPRs, no spills (4 waves: 128 VGPRs, 41 spilled; c5 34.3 -> 31.1 us)
+#endif
+__global__ __launch_bounds__(QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {

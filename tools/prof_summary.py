@@ -13,8 +13,8 @@ Writes, next to the runs:
 each tagged with the bench run's own workload state (mean live bullets,
 resets per launch, from the JSON line the profiled run printed), which
 bench.py checks before quoting them.  The one-tick step kernel is
-astro_step_quad_kernel<..., MULTI=false, ...> (Lb0E) or astro_step_kernel;
-rollouts (Lb1E) and the other kernels are left out.
+astro_step_quad_kernel<..., MULTI = false, ...> or astro_step_kernel;
+rollouts (MULTI = true) and the other kernels are left out.
 """
 import csv
 import json
@@ -24,7 +24,10 @@ import sys
 
 
 def is_step(name):
-    return ('astro_step_quad_kernel' in name and 'Lb0E' in name) or 'astro_step_kernel' in name
+    # demangled: astro_step_quad_kernel<float, 2, 4, false, 2> (MULTI = false)
+    if 'astro_step_quad_kernel<' in name:
+        return name.split('<', 1)[1].split(',')[3].strip() == 'false'
+    return 'astro_step_kernel<' in name
 
 
 def bench_line(path):
