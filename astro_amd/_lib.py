@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
@@ -65,14 +65,21 @@ class AstroState(ctypes.Structure):
 class AstroPolicy(ctypes.Structure):
     _fields_ = [
         ('kind', ctypes.c_int32),
-        ('reserved', ctypes.c_int32),
+        ('bots', ctypes.c_int32),
         ('seed', ctypes.c_uint64),
         ('tick0', ctypes.c_int64),
         ('env_offset', ctypes.c_int64),
+        ('script_r2', ctypes.c_double),
+        ('script_threshold', ctypes.c_double),
+        ('ship_thrust', ctypes.c_double),
+        ('ship_rspeed', ctypes.c_double),
+        ('bullet_speed', ctypes.c_double),
+        ('ship_radius', ctypes.c_double),
     ]
 
 
-POLICIES = {'control': 0, 'nothing': 1, 'random': 2}
+POLICIES = {'control': 0, 'nothing': 1, 'random': 2, 'bots': 3}
+BOTS = {'nothing': 0, 'script': 1, 'random': 2}
 
 _SYMBOLS = {
     'astro_abi_version': (ctypes.c_int, []),
@@ -86,6 +93,8 @@ _SYMBOLS = {
                                          ctypes.c_void_p]),
     'astro_keytable_build': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_void_p]),
+    'astro_controls': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
+                                      ctypes.POINTER(AstroPolicy), ctypes.c_void_p, ctypes.c_void_p]),
     'astro_features': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     'astro_rollout': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),

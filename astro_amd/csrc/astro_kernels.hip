@@ -757,14 +757,22 @@ struct TickDriver {
     uint64_t seed;           // ASTRO_POLICY_RANDOM
     int64_t tick0;           // ASTRO_POLICY_RANDOM: number of the launch's first tick
     int64_t env_offset;      // ASTRO_POLICY_RANDOM: global id of env 0
+    int32_t bots;            // ASTRO_POLICY_BOTS: ship s's bot = (bots >> 4s) & 15
+    double script_r2, script_threshold, ship_thrust, ship_rspeed, bullet_speed, ship_radius;
 };
 
+__device__ __forceinline__ int ship_bot(const TickDriver &d, int s) {
+    return d.policy == ASTRO_POLICY_BOTS ? (d.bots >> (4 * s)) & 15
+         : d.policy == ASTRO_POLICY_RANDOM ? int(ASTRO_BOT_RANDOM) : int(ASTRO_BOT_NOTHING);
+}
+
 // Control of ship s of env i at tick kt of the launch.  RANDOM is uniform in
-// [0, 6) from splitmix64(global ship id, tick) -- bench.py's `controls`.
+// [0, 6) from splitmix64(global ship id, tick) -- bench.py's `controls`.  A
+// ScriptBot ship gets 2 here; its decision needs the state (script_control).
 template <int S>
 __device__ __forceinline__ int tick_control(const TickDriver &d, int i, int s, size_t n_env, int kt) {
     if (d.policy == ASTRO_POLICY_CONTROL) return int(d.control[(size_t(kt) * n_env + size_t(i)) * S + s]);
-    if (d.policy == ASTRO_POLICY_RANDOM) {
+    if (ship_bot(d, s) == ASTRO_BOT_RANDOM) {
         const uint64_t id = uint64_t(d.env_offset + i) * uint64_t(S) + uint64_t(s);
         uint64_t z = id * 0x9E3779B97F4A7C15ull + uint64_t(d.tick0 + kt + 1) * 0xD1B54A32D192ED03ull + d.seed;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -772,7 +780,110 @@ __device__ __forceinline__ int tick_control(const TickDriver &d, int i, int s, s
         z ^= z >> 31;
         return int(((z >> 32) * 6ull) >> 32);
     }
-    return 2;   // ASTRO_POLICY_NOTHING: script.NothingBot
+    return 2;   // script.NothingBot
+}
+
+// ---------------------------------------------------------------------------
+// script.ScriptBot (script.py:13-91) on the bot's ego view (core.roll_ships:
+// its own ship first), in the precision numpy evaluates it for the state's
+// dtypes (NEP 50: Python-float constants take the array's dtype):
+//   X -- ship positions, velocities and bearings, and ship - planet
+//        positions: float32 at a game's first tick (create()'s arrays),
+//        float64 after;
+//   V -- ship - planet velocities: float32 only at the first tick of a
+//        one-planet game (its planet's dx is float32 for ever), else float64.
+// Scalar ** 2 in the reference is pow(x, 2); x * x here (they differ only
+// where pow is not correctly rounded).
+
+// util.norm_angle (util.py:125-132): ((b + pi) % (2 pi)) - pi with numpy's
+// floored remainder (npy_divmod: fmod, + divisor when the signs differ, +0
+// for a zero result), in C
+template <typename C>
+__device__ __forceinline__ C np_norm_angle(C b) {
+    const C pi = C(3.141592653589793);          // np.pi (float32: 3.1415927f)
+    const C two_pi = C(6.283185307179586);      // 2 * np.pi
+    const C x = b + pi;
+    C m = fmod(x, two_pi);
+    m = m != C(0) ? (m < C(0) ? m + two_pi : m) : C(0);
+    return m - pi;
+}
+
+__device__ __forceinline__ float np_atan2(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double np_atan2(double y, double x) { return atan2(y, x); }
+
+// ScriptBot._fly_to (script.py:26-35); t is a value of the angle's dtype
+template <typename C>
+__device__ __forceinline__ int fly_to(C target, C bearing, C t, bool fwd) {
+    const C angle = np_norm_angle<C>(target - bearing);
+    if (angle < -t) return 0;   // rotate left
+    if (t < angle) return 4;    // rotate right
+    return fwd ? 3 : 2;
+}
+
+// ScriptBot._danger (script.py:37-62) for one planet: true with the bearing
+// to steer for when the course meets the inflated planet soon.  (As in the
+// reference, `b` is rebound to the quadratic's linear coefficient before the
+// rotation estimate uses it.)
+template <typename X, typename V>
+__device__ __forceinline__ bool script_danger(const TickDriver &d, X rx, X ry, V rvx, V rvy, X &steer) {
+    using L = typename std::conditional<(sizeof(X) >= sizeof(V)), X, V>::type;
+    const V speed = sqrt(rvx * rvx + rvy * rvy);            // util.mag(dx)
+    const V den = speed + V(1e-12);                          // util.norm(dx)
+    const V nx = rvx / den, ny = rvy / den;
+    const L lin = L(2) * (L(nx) * L(rx) + L(ny) * L(ry));   // 2 * util.dot(norm(dx), x)
+    const X mag = sqrt(rx * rx + ry * ry);
+    const X c = mag * mag - X(d.script_r2);
+    const L det = lin * lin - L(X(4) * c);
+    if (!(L(0) < det)) return false;
+    const L sq = sqrt(det);
+    if (!(L(0) <= -lin + sq)) return false;
+    const L distance = -lin - sq;
+    const X bx = np_atan2(rx, ry);                           // util.bearing(x)
+    const L rotation = fabs(np_norm_angle<L>(L(bx) - lin));
+    const L reach = (L(speed / V(d.ship_thrust)) + L(d.ship_rspeed) / rotation) * L(speed);
+    if (!(distance < reach)) return false;
+    steer = bx;
+    return true;
+}
+
+// ScriptBot.__call__ (script.py:64-91): (m*) the bot's own ship, (e*) the
+// other ship (two-ship games), planets j < np
+template <typename X, typename V, int S, int PMAX>
+__device__ __forceinline__ int script_decide(const TickDriver &d, bool solo, int np, const double (&px)[PMAX],
+                                          const double (&py)[PMAX], const double (&pdx)[PMAX],
+                                          const double (&pdy)[PMAX], double mx, double my, double mdx,
+                                          double mdy, double mb, double ex, double ey, double edx, double edy) {
+    for (int j = 0; j < PMAX; ++j) {   // don't crash into planets (in index order)
+        X steer;
+        if (j < np && script_danger<X, V>(d, X(mx) - X(px[j]), X(my) - X(py[j]), V(mdx) - V(pdx[j]),
+                                          V(mdy) - V(pdy[j]), steer))
+            return fly_to<X>(steer, X(mb), X(d.script_threshold), true);
+    }
+    if (S == 1 || solo) return 2;      // no enemy to aim for
+    // aim for the enemy: where it will be when a bullet gets there
+    const X dx = X(ex) - X(mx), dy = X(ey) - X(my);
+    const X distance = sqrt(dx * dx + dy * dy);
+    const X flight = distance / X(d.bullet_speed);
+    const X fx = X(ex) + flight * (X(edx) - X(mdx));
+    const X fy = X(ey) + flight * (X(edy) - X(mdy));
+    return fly_to<X>(np_atan2(fx - X(mx), fy - X(my)), X(mb), X(d.ship_radius) / distance, false);
+}
+
+// dtype dispatch: X float32 at tick 0, V float32 at tick 0 of a one-planet game
+template <int S, int PMAX>
+__device__ __forceinline__ int script_control(const TickDriver &d, bool solo, bool t0, int np,
+                                              const double (&px)[PMAX], const double (&py)[PMAX],
+                                              const double (&pdx)[PMAX], const double (&pdy)[PMAX], double mx,
+                                              double my, double mdx, double mdy, double mb, double ex, double ey,
+                                              double edx, double edy) {
+    if (!t0)
+        return script_decide<double, double, S, PMAX>(d, solo, np, px, py, pdx, pdy, mx, my, mdx, mdy, mb, ex, ey,
+                                                      edx, edy);
+    if (np == 1)
+        return script_decide<float, float, S, PMAX>(d, solo, np, px, py, pdx, pdy, mx, my, mdx, mdy, mb, ex, ey,
+                                                    edx, edy);
+    return script_decide<float, double, S, PMAX>(d, solo, np, px, py, pdx, pdy, mx, my, mdx, mdy, mb, ex, ey,
+                                                 edx, edy);
 }
 constexpr int BCHUNK = 8;  // bullets loaded per batch: 8 loads in flight per lane
 
@@ -981,6 +1092,15 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             buf[u] = bullets[size_t(i) * BC + k];
         }
         n_pl = uint32_t(np);
+        if (drv.policy == ASTRO_POLICY_BOTS) {   // ScriptBot ships decide on the old state
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const int o = S - 1 - s;
+                if (ship_bot(drv, s) == ASTRO_BOT_SCRIPT)
+                    ctl[s] = script_control<S, PMAX>(drv, p.solo != 0, t0, np, px, py, pdx, pdy, sx[s], sy[s],
+                                                     sdx[s], sdy[s], sb[s], sx[o], sy[o], sdx[o], sdy[o]);
+            }
+        }
 
         // ---- ship acceleration (core.py:234-239): thrust along direction(b)
         //      + gravity; floored //2 and %2 of the control code
@@ -1515,7 +1635,7 @@ struct QuadCounts {
 #endif
 
 // One tick of the quad kernel's wave (16 envs), tick kt of the launch.
-template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false>
+template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false>
 __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
                                                 float *__restrict__ reward_all, uint8_t *__restrict__ done_all,
                                                 bool stats, int auto_reset, int kt STAMP_ARG) {
@@ -1563,7 +1683,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
     const V sv = ships[size_t(sq) * NN + i];
     const T sbv = ships_b[size_t(sq) * NN + i];
-    const int ctl = tick_control<S>(drv, i, sq, NN, kt);
+    int ctl = tick_control<S>(drv, i, sq, NN, kt);
     V pv[PPL];
     T mpx[PPL], mpy[PPL];
 #pragma unroll
@@ -1635,6 +1755,25 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // ---- own ship (lanes < S): direction, thrust + gravity (core.py:234-239)
     const double mx = double(sv.x), my = double(sv.y), mdx = double(sv.z), mdy = double(sv.w);
     const double mb = double(sbv);
+    if constexpr (BOTS) {   // (the ScriptBot instance) ScriptBot ships decide on the old state
+        if (drv.policy == ASTRO_POLICY_BOTS) {   // uniform
+            double pdx[PMAX], pdy[PMAX];
+            T mpdx[PPL], mpdy[PPL];
+#pragma unroll
+            for (int m = 0; m < PPL; ++m) {
+                mpdx[m] = pv[m].z;
+                mpdy[m] = pv[m].w;
+            }
+            bcast_slots<T, PPL, LPE>(mpdx, pdx);
+            bcast_slots<T, PPL, LPE>(mpdy, pdy);
+            const double d0x = double(quad_bcast<0, LPE>(sv.z)), d0y = double(quad_bcast<0, LPE>(sv.w));
+            const double d1x = double(quad_bcast<S - 1, LPE>(sv.z)), d1y = double(quad_bcast<S - 1, LPE>(sv.w));
+            const int oe = q == 0 ? S - 1 : 0;   // the other ship
+            if (q < S && ship_bot(drv, q) == ASTRO_BOT_SCRIPT)
+                ctl = script_control<S, PMAX>(drv, p.solo != 0, t0, np, px, py, pdx, pdy, mx, my, mdx, mdy, mb,
+                                              sx[oe], sy[oe], oe == 0 ? d0x : d1x, oe == 0 ? d0y : d1y);
+        }
+    }
     float ds, dc;
 #ifdef ASTRO_ABLATE_SINCOS   // timing ablation only (wrong results)
     ds = float(mb);
@@ -2184,7 +2323,7 @@ struct QuadArgs {
 typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 
-template <typename T, int S, int PMAX, bool MULTI, int LPE>
+template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false>
 #ifndef ASTRO_P8_WAVES
 #define ASTRO_P8_WAVES 3   // 8 planet slots: 141 VGPRs, no spills (4 waves: 128 VGPRs, 41 spilled; c5 34.3 -> 31.1 us)
 #endif
@@ -2216,7 +2355,8 @@ __global__ __launch_bounds__(QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)
             auto kp = __builtin_amdgcn_kernarg_segment_ptr();
             asm volatile("" : "+s"(kp));
             const QuadArgs &a = *(const QuadArgs *)(KernArgs(kp));
-            c = quad_tick<T, S, PMAX, LPE, true>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr, a.auto_reset, kt);
+            c = quad_tick<T, S, PMAX, LPE, true, BOTS>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr,
+                                                        a.auto_reset, kt);
         } else {
             c = quad_tick<T, S, PMAX, LPE>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, kt);
         }
@@ -2241,12 +2381,7 @@ __global__ __launch_bounds__(QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)
 // (npy_divmod: fmod, + divisor when the signs differ, +0 for a zero result)
 template <typename C>
 __device__ __forceinline__ C norm_angle_over_pi(C b) {
-    const C pi = C(3.141592653589793);          // np.pi (float32: 3.1415927f)
-    const C two_pi = C(6.283185307179586);      // 2 * np.pi
-    const C x = b + pi;
-    C m = fmod(x, two_pi);
-    m = m != C(0) ? (m < C(0) ? m + two_pi : m) : C(0);
-    return (m - pi) / pi;
+    return np_norm_angle<C>(b) / C(3.141592653589793);
 }
 
 // A block covers 256 consecutive (env, row) items: the per-env part (every
@@ -2442,6 +2577,36 @@ int check_params(const AstroParams *p) {
     return 0;
 }
 
+int check_policy(const AstroPolicy *q, int nships) {
+    if (q->kind < ASTRO_POLICY_CONTROL || q->kind > ASTRO_POLICY_BOTS)
+        return fail(-71, "policy kind must be CONTROL, NOTHING, RANDOM or BOTS");
+    if (q->kind == ASTRO_POLICY_BOTS) {
+        for (int s = 0; s < nships; ++s) {
+            const int b = (q->bots >> (4 * s)) & 15;
+            if (b != ASTRO_BOT_NOTHING && b != ASTRO_BOT_SCRIPT && b != ASTRO_BOT_RANDOM)
+                return fail(-75, "bot of ship %d must be ASTRO_BOT_NOTHING, _SCRIPT or _RANDOM", s);
+        }
+    }
+    return 0;
+}
+
+TickDriver driver_of(const AstroPolicy &q, int ticks) {
+    TickDriver d{};
+    d.policy = q.kind;
+    d.ticks = ticks;
+    d.seed = q.seed;
+    d.tick0 = q.tick0;
+    d.env_offset = q.env_offset;
+    d.bots = q.bots;
+    d.script_r2 = q.script_r2;
+    d.script_threshold = q.script_threshold;
+    d.ship_thrust = q.ship_thrust;
+    d.ship_rspeed = q.ship_rspeed;
+    d.bullet_speed = q.bullet_speed;
+    d.ship_radius = q.ship_radius;
+    return d;
+}
+
 int launched(const char *what) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(-1000 - int(e), "%s launch failed: %s", what, hipGetErrorString(e));
@@ -2473,13 +2638,20 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
     if (kind == ASTRO_KERNEL_QUAD || kind == ASTRO_KERNEL_PAIR) {   // all ticks in one launch
         const int lpe = kind == ASTRO_KERNEL_QUAD ? 4 : 2;
         const int grid = int((int64_t(s.n_env) * lpe + QBLOCK - 1) / QBLOCK);
-        if (lpe == 4 && drv.ticks == 1)
+        const bool one = drv.ticks == 1;
+        if (drv.policy == ASTRO_POLICY_BOTS) {   // ScriptBot code lives in its own (pair) instance only
+            const int g2 = int((int64_t(s.n_env) * 2 + QBLOCK - 1) / QBLOCK);
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 2, true>), dim3(g2), dim3(QBLOCK), 0, stream,
+                               p, s, drv, r, d, st, ar);
+            return launched("astro_step(pair, bots)");
+        }
+        if (lpe == 4 && one)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);
         else if (lpe == 4)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);
-        else if (drv.ticks == 1)
+        else if (one)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);
         else
@@ -2512,6 +2684,48 @@ int launch_reset(const AstroParams &p, const AstroState &s, const uint32_t *seed
     const int grid = (s.n_env + BLOCK - 1) / BLOCK;
     hipLaunchKernelGGL((astro_reset_kernel<T, S, PM>), dim3(grid), dim3(BLOCK), 0, stream, p, s, seeds, mask);
     return launched("astro_reset");
+}
+
+// core.Bots.control for every env (astro_controls): one lane per env reads the
+// state and runs each ship's bot, as the step kernels do at a tick's start
+template <typename T, int S, int PMAX>
+__global__ __launch_bounds__(BLOCK) void astro_controls_kernel(AstroParams p, AstroState st, TickDriver drv,
+                                                               int8_t *__restrict__ out) {
+    using V = typename Store<T>::V;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= st.n_env) return;
+    const size_t NN = size_t(st.n_env);
+    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+    const int tick = int(uint32_t(h.x) & TICK_MASK);
+    int np = h.y & 0xff;
+    np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+    double sx[S], sy[S], sdx[S], sdy[S], sb[S], px[PMAX], py[PMAX], pdx[PMAX], pdy[PMAX];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const V v = reinterpret_cast<const V *>(st.ships)[size_t(s) * NN + i];
+        sx[s] = double(v.x);
+        sy[s] = double(v.y);
+        sdx[s] = double(v.z);
+        sdy[s] = double(v.w);
+        sb[s] = double(reinterpret_cast<const T *>(st.ships_b)[size_t(s) * NN + i]);
+    }
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) {
+        const V v = reinterpret_cast<const V *>(st.planets)[size_t(j < p.p_pad ? j : 0) * NN + i];
+        px[j] = double(v.x);
+        py[j] = double(v.y);
+        pdx[j] = double(v.z);
+        pdy[j] = double(v.w);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        int c = tick_control<S>(drv, i, s, NN, 0);
+        const int o = S - 1 - s;
+        if (ship_bot(drv, s) == ASTRO_BOT_SCRIPT)
+            c = script_control<S, PMAX>(drv, p.solo != 0, tick == 0, np, px, py, pdx, pdy, sx[s], sy[s], sdx[s],
+                                        sdy[s], sb[s], sx[o], sy[o], sdx[o], sdy[o]);
+        out[size_t(i) * S + s] = int8_t(c);
+    }
 }
 
 // dispatch over (storage type, ships, planet register capacity)
@@ -2547,6 +2761,14 @@ struct StepL {
     }
 };
 template <typename T, int S, int PM>
+struct CtlL {
+    static int run(const AstroParams &p, const AstroState &s, const TickDriver &drv, int8_t *out, hipStream_t st) {
+        hipLaunchKernelGGL((astro_controls_kernel<T, S, PM>), dim3((s.n_env + BLOCK - 1) / BLOCK), dim3(BLOCK), 0,
+                           st, p, s, drv, out);
+        return launched("astro_controls");
+    }
+};
+template <typename T, int S, int PM>
 struct ResetL {
     static int run(const AstroParams &p, const AstroState &s, const uint32_t *seeds, const uint8_t *mask,
                    hipStream_t st) {
@@ -2574,7 +2796,10 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
         return fail(-32, "control must be 2-byte and reward 8-byte aligned");
     if (int64_t(s->n_env) * 4 > int64_t(0x7fffffff)) return fail(-34, "n_env too large");
     if (stats && (reinterpret_cast<uintptr_t>(stats) & 7u)) return fail(-33, "stats must be 8-byte aligned");
-    const TickDriver drv{control, ASTRO_POLICY_CONTROL, 1, 0, 0, 0};
+    TickDriver drv{};
+    drv.control = control;
+    drv.policy = ASTRO_POLICY_CONTROL;
+    drv.ticks = 1;
     return dispatch<StepL>(*p, *s, drv, reward, done, stats, int(auto_reset), reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -2585,8 +2810,7 @@ int astro_rollout(const AstroParams *p, const AstroState *s, const AstroPolicy *
     if (rc) return rc;
     if ((rc = check_state(s))) return rc;
     if (!policy) return fail(-70, "policy is NULL");
-    if (policy->kind < ASTRO_POLICY_CONTROL || policy->kind > ASTRO_POLICY_RANDOM)
-        return fail(-71, "policy kind must be CONTROL, NOTHING or RANDOM");
+    if ((rc = check_policy(policy, p->nships))) return rc;
     if (ticks < 1) return fail(-72, "ticks must be >= 1");
     if (s->n_env == 0) return 0;
     if (policy->kind == ASTRO_POLICY_CONTROL && !control) return fail(-73, "policy CONTROL needs control");
@@ -2596,8 +2820,22 @@ int astro_rollout(const AstroParams *p, const AstroState *s, const AstroPolicy *
         return fail(-32, "control must be 2-byte and reward 8-byte aligned");
     if (int64_t(s->n_env) * 4 > int64_t(0x7fffffff)) return fail(-34, "n_env too large");
     if (stats && (reinterpret_cast<uintptr_t>(stats) & 7u)) return fail(-33, "stats must be 8-byte aligned");
-    const TickDriver drv{control, policy->kind, ticks, policy->seed, policy->tick0, policy->env_offset};
+    TickDriver drv = driver_of(*policy, ticks);
+    drv.control = control;
     return dispatch<StepL>(*p, *s, drv, reward, done, stats, int(auto_reset), reinterpret_cast<hipStream_t>(stream));
+}
+
+int astro_controls(const AstroParams *p, const AstroState *s, const AstroPolicy *policy, int8_t *control,
+                   void *stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if ((rc = check_state(s))) return rc;
+    if (!policy) return fail(-70, "policy is NULL");
+    if ((rc = check_policy(policy, p->nships))) return rc;
+    if (policy->kind == ASTRO_POLICY_CONTROL) return fail(-71, "astro_controls: CONTROL is not a policy");
+    if (s->n_env == 0) return 0;
+    if (!control) return fail(-74, "control is NULL");
+    return dispatch<CtlL>(*p, *s, driver_of(*policy, 1), control, reinterpret_cast<hipStream_t>(stream));
 }
 
 int astro_reset(const AstroParams *p, const AstroState *s, const uint32_t *seeds, const uint8_t *mask,

@@ -239,14 +239,49 @@ class BatchedEnv:
             planets=self.planets.permute(1, 0, 2), nplanets=self.nplanets,
             bullets=self.bullets, nbullets=self.nbullets, tick=self.tick)
 
-    def rollout(self, ticks, policy='random', seed=0, tick0=0, auto_reset=None, stats=True):
-        """``ticks`` consecutive steps with open-loop controls, in one launch
-        (quad kernel; one per tick for the lane kernel): exactly ``ticks``
-        calls of ``step`` with those controls.  ``policy``: 'random'
-        (bench.py's splitmix64 controls keyed by GLOBAL env id and
-        ``tick0 + k``), 'nothing' (script.NothingBot), or an int8 tensor
-        [ticks, N, S] of controls.  Returns (reward [ticks, N, S],
-        done [ticks, N])."""
+    def policy(self, policy, seed=0, tick0=0, script_args=None):
+        """The AstroPolicy of a policy name: 'random' (bench.py's splitmix64
+        controls keyed by GLOBAL env id and tick), 'nothing'
+        (script.NothingBot), 'script' (script.ScriptBot for every ship), or
+        one bot name per ship, e.g. ('nothing', 'script') -- core.Bots with
+        those bots (core.py:359-363).  script_args: ScriptBot's args
+        (default ScriptBot.DEFAULT_ARGS, script.py:18-21)."""
+        c = self.config
+        a = dict(avoid_distance=0.1, avoid_threshold=0.45)
+        a.update(script_args or {})
+        pol = _lib.AstroPolicy(
+            seed=int(seed), tick0=int(tick0), env_offset=self.env_offset,
+            script_r2=(c.planet_radius + c.ship_radius + a['avoid_distance']) ** 2,
+            script_threshold=float(a['avoid_threshold']), ship_thrust=float(c.ship_thrust),
+            ship_rspeed=float(c.ship_rspeed), bullet_speed=float(c.bullet_speed),
+            ship_radius=float(c.ship_radius))
+        if isinstance(policy, str) and policy in ('random', 'nothing'):
+            pol.kind = _lib.POLICIES[policy]
+            return pol
+        names = [policy] * self.S if isinstance(policy, str) else list(policy)
+        if len(names) != self.S or any(n not in _lib.BOTS for n in names):
+            raise ValueError('policy must be random/nothing/script or one of %s per ship' % sorted(_lib.BOTS))
+        pol.kind = _lib.POLICIES['bots']
+        pol.bots = sum(_lib.BOTS[n] << (4 * s) for s, n in enumerate(names))
+        return pol
+
+    def controls(self, policy='script', seed=0, tick0=0, script_args=None):
+        """core.Bots.control (core.py:359-363) for every env: int8 [N, S]
+        controls ``policy`` (see ``policy``) picks on the current state, each
+        ship on its ego view -- computed on the device (astro_controls)."""
+        out = torch.empty((self.n_env, self.S), dtype=torch.int8, device=self.device)
+        pol = self.policy(policy, seed, tick0, script_args)
+        _lib.check(self.lib.astro_controls(ctypes.byref(self.params), ctypes.byref(self.state), ctypes.byref(pol),
+                                           out.data_ptr(), _stream_ptr(self.device)), 'astro_controls')
+        return out
+
+    def rollout(self, ticks, policy='random', seed=0, tick0=0, auto_reset=None, stats=True, script_args=None):
+        """``ticks`` consecutive steps in one launch (quad/pair kernels; one
+        per tick for the lane kernel): exactly ``ticks`` calls of ``step``
+        with the controls ``policy`` picks each tick -- a policy name (see
+        ``policy``: 'random', 'nothing', 'script', or one bot per ship) or
+        an int8 tensor [ticks, N, S] of controls.  Returns (reward [ticks,
+        N, S], done [ticks, N])."""
         ticks = int(ticks)
         ar = self.auto_reset if auto_reset is None else bool(auto_reset)
         ctl = None
@@ -254,10 +289,9 @@ class BatchedEnv:
             ctl = policy.to(device=self.device, dtype=torch.int8).contiguous()
             if tuple(ctl.shape) != (ticks, self.n_env, self.S):
                 raise ValueError('control must be [%d, %d, %d]' % (ticks, self.n_env, self.S))
-            kind = _lib.POLICIES['control']
+            pol = _lib.AstroPolicy(kind=_lib.POLICIES['control'])
         else:
-            kind = _lib.POLICIES[policy]
-        pol = _lib.AstroPolicy(kind=kind, seed=int(seed), tick0=int(tick0), env_offset=self.env_offset)
+            pol = self.policy(policy, seed, tick0, script_args)
         reward = torch.empty((ticks, self.n_env, self.S), dtype=torch.float32, device=self.device)
         done = torch.empty((ticks, self.n_env), dtype=torch.uint8, device=self.device)
         _lib.check(self.lib.astro_rollout(
@@ -266,6 +300,53 @@ class BatchedEnv:
             self.stats.data_ptr() if stats else None, int(ar), _stream_ptr(self.device)), 'astro_rollout')
         self._keep_rollout = ctl
         return reward, done
+
+    def play(self, bots, games=1, chunk=256, max_ticks=None, script_args=None):
+        """core.play (core.py:377-410) batched: every env plays its next
+        ``games`` games (auto-reset onto its generate_configs stream) with
+        ``bots`` (one name per ship, or one name for all: 'nothing',
+        'script', 'random'), ``chunk`` ticks per astro_rollout launch, from
+        the envs' current states.  Returns (winner int64 [N, games]: -1 for
+        None, else the index of the winning ship -- argmax of the final
+        reward when its max is >= 1, core.py:409 -- and length int64
+        [N, games] in ticks)."""
+        N, G = self.n_env, int(games)
+        winner = torch.full((N, G), -2, dtype=torch.int64, device=self.device)
+        length = torch.zeros((N, G), dtype=torch.int64, device=self.device)
+        got = torch.zeros(N, dtype=torch.int64, device=self.device)
+        start = -self.tick.to(torch.int64)          # tick number at which each env's game began
+        t = 0
+        limit = max_ticks if max_ticks is not None else G * (self.schedule.timeout_tick + 1) + chunk
+        while int(got.min()) < G:
+            if t >= limit:
+                raise RuntimeError('play: games did not finish within %d ticks' % limit)
+            reward, done = self.rollout(chunk, bots, tick0=t, auto_reset=True, script_args=script_args)
+            d = done != 0
+            k, e = torch.nonzero(d, as_tuple=True)          # tick-major: each env's games in order
+            if k.numel():
+                order = torch.argsort(e * chunk + k)
+                k, e = k[order], e[order]
+                # rank of each finish among its env's finishes in this chunk
+                first = torch.ones_like(e, dtype=torch.bool)
+                first[1:] = e[1:] != e[:-1]
+                idx = torch.arange(e.numel(), device=self.device)
+                seg = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
+                g = got[e] + (idx - seg)
+                r = reward[k, e]                              # [M, S]
+                mx, am = r.max(1)
+                w = torch.where(mx >= 1, am, torch.full_like(am, -1))
+                prev_end = torch.where(first, start[e], t + k[torch.clamp(idx - 1, min=0)] + 1)
+                ok = g < G
+                winner[e[ok], g[ok]] = w[ok]
+                length[e[ok], g[ok]] = (t + k + 1 - prev_end)[ok]
+                last = torch.zeros(N, dtype=torch.int64, device=self.device)
+                last.scatter_reduce_(0, e, t + k + 1, reduce='amax', include_self=False)
+                has = torch.zeros(N, dtype=torch.bool, device=self.device)
+                has[e] = True
+                start = torch.where(has, last, start)
+                got += torch.bincount(e, minlength=N)
+            t += chunk
+        return winner, length
 
     def features(self, rows=None, out=None):
         """Observation features of every env, as rl.ValueNetwork.get_features

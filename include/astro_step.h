@@ -11,6 +11,8 @@
  *                         for open-loop / scripted controls, K ticks per launch
  *                         (plus auto-reset = core.create(next config of the
  *                         env's generate_configs stream), core.py:77-135)
+ *   astro_controls     <- core.Bots.control(bots, state)      core.py:359-363
+ *                         with script.NothingBot / ScriptBot  script.py:6-91
  *   astro_reset        <- core.create(config)                 core.py:86-135
  *   astro_stream_init  <- core.generate_configs(config)       core.py:77-83
  *   astro_features     <- rl.ValueNetwork.get_features(state) + to_batch
@@ -38,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 11
+#define ASTRO_ABI_VERSION 12
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -112,20 +114,38 @@ typedef struct AstroState {
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
 } AstroState;
 
-/* Control sources of astro_rollout. */
+/* Control sources of astro_rollout / astro_controls. */
 enum {
     ASTRO_POLICY_CONTROL = 0,  /* a control array, int8 [ticks][n_env][nships] */
     ASTRO_POLICY_NOTHING = 1,  /* script.NothingBot (script.py:6-10): every ship 2 */
-    ASTRO_POLICY_RANDOM = 2    /* uniform [0, 6) per ship and tick: splitmix64 of
+    ASTRO_POLICY_RANDOM = 2,   /* uniform [0, 6) per ship and tick: splitmix64 of
                                   (global ship id, tick) -- bench.py's `controls` */
+    ASTRO_POLICY_BOTS = 3      /* one bot per ship (core.Bots.control, core.py:359-363):
+                                  ship s plays bot (bots >> 4s) & 15, an ASTRO_BOT_*,
+                                  on its ego view of the state (core.roll_ships) */
+};
+enum {
+    ASTRO_BOT_NOTHING = 0,     /* script.NothingBot */
+    ASTRO_BOT_SCRIPT = 1,      /* script.ScriptBot (script.py:13-91): planet avoidance, then
+                                  aim at the enemy's forecast; numpy's precision for the
+                                  state's dtypes (float32 at a game's first tick) */
+    ASTRO_BOT_RANDOM = 2       /* as ASTRO_POLICY_RANDOM for that ship */
 };
 
 typedef struct AstroPolicy {
     int32_t kind;          /* ASTRO_POLICY_* */
-    int32_t reserved;
+    int32_t bots;          /* BOTS: ship s's bot = (bots >> (4 * s)) & 15 */
     uint64_t seed;         /* RANDOM */
     int64_t tick0;         /* RANDOM: number of the first tick */
     int64_t env_offset;    /* RANDOM: global id of env 0 (shards) */
+    /* ASTRO_BOT_SCRIPT: ScriptBot's constants as the reference evaluates them
+       (Python floats; the bot casts them to the state's dtype as numpy does) */
+    double script_r2;        /* (planet_radius + ship_radius + avoid_distance) ** 2   script.py:47-49 */
+    double script_threshold; /* args['avoid_threshold']                               script.py:71 */
+    double ship_thrust;      /* config.ship_thrust                                    script.py:57 */
+    double ship_rspeed;      /* config.ship_rspeed                                    script.py:58 */
+    double bullet_speed;     /* config.bullet_speed                                   script.py:81 */
+    double ship_radius;      /* config.ship_radius                                    script.py:88 */
 } AstroPolicy;
 
 /* Statistics accumulated by astro_step when `stats` is non-NULL: uint64
@@ -167,6 +187,14 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
 int astro_rollout(const AstroParams *p, const AstroState *s, const AstroPolicy *policy, int32_t ticks,
                   const int8_t *control, float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset,
                   void *stream);
+
+/* core.Bots.control (core.py:359-363) for every env: control int8
+ * [n_env][nships] = the controls `policy` picks on the current state (tick
+ * policy->tick0 for RANDOM; CONTROL is not a policy here).  The same device
+ * code astro_rollout runs each tick, for a host loop that needs the
+ * decisions (e.g. to log them) or to check them. */
+int astro_controls(const AstroParams *p, const AstroState *s, const AstroPolicy *policy, int8_t *control,
+                   void *stream);
 
 /* core.create for the envs with mask[i] != 0 (mask NULL = all): from
  * seeds[i] when seeds != NULL, else from the next seed of env i's stream. */

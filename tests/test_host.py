@@ -32,7 +32,8 @@ def _declared_functions():
 def test_library_exports_every_header_symbol(lib):
     names = _declared_functions()
     assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_reset',
-                          'astro_stream_init', 'astro_keytable_build', 'astro_features', 'astro_rollout'}
+                          'astro_stream_init', 'astro_keytable_build', 'astro_features', 'astro_rollout',
+                          'astro_controls'}
     out = subprocess.check_output(['nm', '-D', '--defined-only', _lib.LIB_PATH], text=True)
     exported = set(re.findall(r' T (astro_\w+)$', out, re.M))
     assert set(names) <= exported
@@ -91,10 +92,19 @@ def test_argument_validation_without_gpu(lib):
     assert lib.astro_features(ctypes.byref(p), ctypes.byref(s), None, 0, None) == 0   # empty batch
     s.n_env = 4
     assert lib.astro_features(ctypes.byref(p), ctypes.byref(s), None, 36, None) == -4  # arrays NULL
-    pol = _lib.AstroPolicy(kind=3)
+    pol = _lib.AstroPolicy(kind=4)
     s.n_env = 0
     assert lib.astro_rollout(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), 4, None, None, None,
                              None, 0, None) == -71
+    pol.kind = 3            # BOTS with an unknown bot for ship 1
+    pol.bots = 1 | (7 << 4)
+    assert lib.astro_rollout(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), 4, None, None, None,
+                             None, 0, None) == -75
+    assert lib.astro_controls(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), None, None) == -75
+    pol.bots = 1 | (2 << 4)
+    assert lib.astro_controls(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), None, None) == 0
+    pol.kind = 0            # a control array is not a policy for astro_controls
+    assert lib.astro_controls(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), None, None) == -71
     pol.kind = 2
     assert lib.astro_rollout(ctypes.byref(p), ctypes.byref(s), ctypes.byref(pol), 0, None, None, None,
                              None, 0, None) == -72
