@@ -227,6 +227,17 @@ class BatchedEnv:
     def nbullets(self):
         return (self.hdr[:, 1] >> 16) & 0xffff
 
+    def info(self):
+        """Per-env flags of the last step (SURVEY section 8b's info): ``hit``
+        uint8 bitmask of the ships a collision hit (bit s: reward[s] == -1 on
+        a collision, core.py:253-255), ``overflow`` the env's current game
+        has dropped a bullet for lack of b_cap, ``create_exhausted`` its
+        create() needed more than 227 MT19937 words (never in practice)."""
+        hit = ((self.reward < 0) & (self.done == 1)[:, None]).to(torch.uint8)
+        hit = (hit << torch.arange(self.S, device=self.device, dtype=torch.uint8)[None, :]).sum(1)
+        fl = self.flags
+        return dict(hit=hit.to(torch.uint8), overflow=(fl & 1) != 0, create_exhausted=(fl & 2) != 0)
+
     @property
     def game_seed(self):
         """Config.seed of each env's current game."""

@@ -558,3 +558,34 @@ def test_rollout_device_policies(kernel):
     rew, done = a.rollout(K, 'nothing')
     rew_b, done_b = b.rollout(K, torch.full((K, n, 2), 2, dtype=torch.int8, device='cuda:0'))
     assert torch.equal(rew, rew_b) and torch.equal(done, done_b) and torch.equal(a.planets, b.planets)
+
+
+def test_step_info_flags():
+    """BatchedEnv.info(): the hit bitmask of a collision step equals the
+    reference's 1 - 2 * hit rewards (core.py:253-255), and the overflow flag
+    of each env equals the oracle's dropped-bullet flag (small b_cap)."""
+    cfg = CFG['rapid']
+    P = batched.make_params(cfg)
+    n = 517
+    env = _env(cfg, n, dtype=torch.float32, b_cap=6, auto_reset=False)
+    env.reset()
+    rng = np.random.RandomState(3)
+    saw_hit = saw_over = False
+    for t in range(40):
+        B = _host_batch(env)
+        ctl = rng.randint(0, 6, size=(n, 2)).astype(np.int8)
+        want, wrew, wdone = batched.step(B, ctl, P, store='f32')
+        env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+        info = env.info()
+        hit = info['hit'].cpu().numpy()
+        coll = wdone == 1
+        want_hit = ((wrew < 0) & coll[:, None]).astype(np.uint8) @ np.array([1, 2], np.uint8)
+        assert np.array_equal(hit, want_hit), t
+        run = wdone == 0
+        assert np.array_equal(info['overflow'].cpu().numpy()[run], want.overflow[run]), t
+        assert not info['create_exhausted'].cpu().numpy().any()
+        saw_hit |= bool(hit.any())
+        saw_over |= bool(want.overflow[run].any())
+        if (~run).any():
+            env.reset(mask=torch.from_numpy((~run).astype(np.uint8)).cuda())
+    assert saw_hit and saw_over
