@@ -50,6 +50,15 @@ namespace {
 struct alignas(16) F4 { float x, y, z, w; };
 struct alignas(16) D4 { double x, y, z, w; };
 
+// 16 bytes at base + 16 i through a global (not flat) pointer: for an address
+// chosen between arrays at run time (a flat load would make the compiler
+// wait for every load before it, flat ones completing out of order)
+__device__ __forceinline__ uint4 load_u4_global(uintptr_t base, size_t i) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u v = *reinterpret_cast<const __attribute__((address_space(1))) v4u *>(base + 16 * i);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 template <typename T> struct Store;
 template <> struct Store<float> { using V = F4; };
 template <> struct Store<double> { using V = D4; };
@@ -738,11 +747,18 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
             stamp_[k == 0 ? 12 : 13] = t_;                                                \
         }                                                                                \
     } while (0)
-constexpr int NSTAMP = 16;
+constexpr int NSTAMP = 24;   // 0-13 step sections, 14-15 placement, 16-19 reset pass
 #else
 #define STAMP(k) \
     do {         \
     } while (0)
+#endif
+#ifdef ASTRO_STAMPS
+#define STAMP_ARG , unsigned long long *stamp_
+#define STAMP_PASS , stamp_
+#else
+#define STAMP_ARG
+#define STAMP_PASS
 #endif
 
 constexpr int BLOCK = 64;
@@ -1083,8 +1099,11 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         // key[397] of the next game's seed, fetched once per game, off the reset path
         uint32_t pend_key = uint32_t(h.w);
         if (!key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
-        uint4 c_pend = make_uint4(0u, 0u, 0u, 0u);   // stream cursor, for check_pending
-        if (!key_valid && p.key_table && p.planets_only) c_pend = reinterpret_cast<const uint4 *>(st.stream)[i];
+        // stream cursor, for check_pending: loaded branch-free, see the quad kernel
+        const bool want_c = !key_valid && p.key_table && p.planets_only;
+        uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
+        asm volatile("" : "+v"(c_stream), "+v"(c_hdr));
+        const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
         V buf[BCHUNK];
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) {
@@ -1534,7 +1553,7 @@ template <typename T, int S, int PMAX, int LPE>
 __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
                                                     int lane, int i, uint32_t pend_seed, uint32_t pend_key,
                                                     bool have_key, uint32_t (*s_chain)[2][13 + 2 * S],
-                                                    int *s_serial) {
+                                                    int *s_serial STAMP_ARG) {
     constexpr int NW = 12 + 2 * S;   // outputs create() draws, randint accepting its first word
     int leader[4];
 #pragma unroll
@@ -1570,6 +1589,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     wave_sync();   // s_chain is free for the next pass
     const uint32_t y = (a0 & 0x80000000u) | (a1 & 0x7fffffffu);
     const uint32_t w = mt_temper(b0 ^ (y >> 1) ^ ((a1 & 1u) ? 0x9908b0dfu : 0u));   // output u
+    STAMP(16);
 
     // randint(1, max_planets + 1) on output 0
     const uint32_t rng = uint32_t(p.max_planets - 1);
@@ -1600,6 +1620,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     d.u_base = many ? r_base : 0.0;
     d.reverse = many && (w_rev & 1u) == 0 ? -1 : 1;
     d.exhausted = false;   // NW outputs, far below the 227 the lazy generator covers
+    STAMP(17);
 
     int n, cf = 0;
     if constexpr (2 * PMAX + 1 <= 16) {
@@ -1607,6 +1628,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     } else {
         if (on && fast) n = create_env<T, S, PMAX, 16>(p, st, ie, d, cf, u);
     }
+    STAMP(18);
     if (on && fast) {
         if (u == 0) {   // the stream record and header, as restart_env
             MTStream g{c.x, c.y, c.z, stream_ring_of(st, ie)};
@@ -1616,6 +1638,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
         }
     }
     if (on && !fast && u == 0) s_serial[L / LPE] = 1;
+    STAMP(19);
     return todo;
 }
 
@@ -1626,13 +1649,6 @@ struct QuadCounts {
     uint32_t c_serial;                      // per wave: resets by the serial create
 };
 
-#ifdef ASTRO_STAMPS
-#define STAMP_ARG , unsigned long long *stamp_
-#define STAMP_PASS , stamp_
-#else
-#define STAMP_ARG
-#define STAMP_PASS
-#endif
 
 // One tick of the quad kernel's wave (16 envs), tick kt of the launch.
 template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false>
@@ -1738,8 +1754,16 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // gather into the 4 GiB key table, issued after every load the physics
     // waits for, so only its consumers (header store, reset) wait for it
     if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
-    uint4 c_pend = make_uint4(0u, 0u, 0u, 0u);   // stream cursor, for check_pending
-    if (q == 0 && !key_valid && p.key_table && p.planets_only) c_pend = reinterpret_cast<const uint4 *>(st.stream)[i];
+    // stream cursor, for check_pending (read there under this same condition
+    // only).  Every lane loads, the others their own header again (the line
+    // just read: no traffic).  A conditional load made the compiler merge
+    // its value with the other lanes' zeros right after it, i.e. wait for it
+    // -- and for every load before it, the key-table gather included -- at
+    // the top of the wave (c3 13.10 -> 12.65 us, c2 6.74 -> 6.64 us, A/B)
+    const bool want_c = q == 0 && !key_valid && p.key_table && p.planets_only;
+    uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
+    asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // values, not a select between the fields' addresses
+    const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
 
     // ---- quad broadcasts: all planets, both ships
     double px[PMAX], py[PMAX], sx[S], sy[S];
@@ -2252,7 +2276,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     //      randint words (max_planets not a power of two) take the serial path
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
         todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
-                                           s_chain, s_serial);
+                                           s_chain, s_serial STAMP_PASS);
     if (auto_reset) {
         wave_sync();
         if (stats) c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));

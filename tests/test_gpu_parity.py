@@ -184,6 +184,32 @@ def test_step_teacher_forced_vs_reference(fname, dtype, kernel):
                      rounding=dtype == torch.float32)
 
 
+@pytest.mark.parametrize('kernel', KERNELS)
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+def test_planets_only_handmade_states(dtype, kernel):
+    """With planets_only=3 the step kernels do not read planet slots >= 3 (a
+    filtered game never has a planet there); a hand-made state that does --
+    here the reference's own 1-4 planet transitions -- must still step
+    exactly: the kernel reads those slots once the header says so."""
+    tr = gio.Transitions('steps.npz')
+    idx = [i for name, i in tr.groups() if name == 'default'][0]
+    cfg = CFG['default']
+    bcap = tr.max_bullets(idx) + 2
+    B = tr.batch_in(idx, 2, p_pad=4, b_cap=bcap)
+    assert (B.nplanets == 4).any() and (B.nplanets < 4).any()
+    from astro_amd import BatchedEnv
+    env = BatchedEnv(cfg, idx.size, device='cuda:0', b_cap=bcap, p_pad=4, dtype=dtype, auto_reset=False,
+                     kernel=kernel, planets_only=3)
+    env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
+    ctl = tr.z['control'][idx, :2].astype(np.int8)
+    _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+    E, erew, edone = tr.expected(idx, 2, p_pad=4, b_cap=bcap)
+    done = done.cpu().numpy()
+    assert (done == edone).all()
+    assert np.array_equal(rew.cpu().numpy(), erew.astype(np.float32))
+    _assert_same('planets_only handmade', _host_batch(env), E, done == 0, rounding=dtype == torch.float32)
+
+
 # ------------------------------------------------------- free-running games
 
 @pytest.mark.parametrize('kernel', KERNELS)

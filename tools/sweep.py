@@ -47,6 +47,9 @@ def run(name, cfg, n, ticks=200, warm=150, b_cap=32, p_pad=4, auto_reset=True, s
                           planets_per_env=d['planets'] / n)), flush=True)
 
 
+NSTAMP = 24   # the kernel's NSTAMP (stamp words per wave row)
+
+
 def use_lib(name):
     from astro_amd import _lib
     _lib._lib = None
@@ -54,15 +57,15 @@ def use_lib(name):
 
 
 def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hip_stamps.so',
-           kernel='lane'):
+           kernel='lane', auto_reset=True):
     """Per-section cycle shares from the -DASTRO_STAMPS diagnostic library."""
     from astro_amd import _lib
     use_lib(lib)
-    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, kernel=kernel)
+    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, kernel=kernel, auto_reset=auto_reset)
     env.reset()
     nw = (n + 63) // 64 if kernel == 'lane' else ((n + 31) // 32 if kernel == 'pair' else (n + 15) // 16)
     ncr = 0
-    env.stats = torch.zeros(nw + ncr, 16, dtype=torch.int64, device='cuda')
+    env.stats = torch.zeros(nw + ncr, NSTAMP, dtype=torch.int64, device='cuda')
     ctl = torch.from_numpy(bench.controls(0, n, env.S, warm + ticks)).cuda()
     for t in range(warm):
         env.launch(ctl[t].data_ptr(), stats=False)
@@ -72,9 +75,9 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
         env.launch(ctl[warm + t].data_ptr(), stats=True)
         torch.cuda.synchronize()
         rows.append(env.stats.cpu().numpy().astype(np.int64))
-    R = np.stack(rows, 0)            # [ticks, nw + ncr, 16]
+    R = np.stack(rows, 0)            # [ticks, nw + ncr, NSTAMP]
     C = R[:, nw:, :]                 # creator rows
-    S = R[:, :nw, :].reshape(-1, 16)
+    S = R[:, :nw, :].reshape(-1, NSTAMP)
     s0 = S[:, 0]
     tot = S[:, 11] - s0
     out = dict(name=name, n=n, wave_cycles_mean=float(tot.mean()), wave_cycles_max=float(tot.max()))
@@ -96,6 +99,18 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
     out['sclk_mhz'] = float((tot / np.maximum(rt, 1)).mean() * 100.0)
     out['wave_us_max'] = float(rt.max() / 100.0)
     out['wave_us_mean'] = float(rt.mean() / 100.0)
+    # per launch: wave start / end relative to the launch's first wave start (100 MHz clock)
+    rows_per = len(S) // ticks
+    st_rel, en_rel = [], []
+    for t in range(ticks):
+        sl = slice(t * rows_per, (t + 1) * rows_per)
+        t0w = S[sl, 12].min()
+        st_rel.append((S[sl, 12] - t0w) / 100.0)
+        en_rel.append((S[sl, 13] - t0w) / 100.0)
+    st_rel, en_rel = np.concatenate(st_rel), np.concatenate(en_rel)
+    out['wave_start_us'] = dict(mean=float(st_rel.mean()), p90=float(np.percentile(st_rel, 90)), max=float(st_rel.max()))
+    out['wave_end_us'] = dict(mean=float(en_rel.mean()), p90=float(np.percentile(en_rel, 90)),
+                              launch_mean=float(np.mean([e.max() for e in np.split(en_rel, ticks)])))
     if ncr:
         t0 = R[:, :nw, 12].min(1)[:, None].astype(np.float64)
         cs, cl, ce = [(C[:, :, k] - t0) / 100.0 for k in (0, 1, 2)]
@@ -142,6 +157,13 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
         out['simd_top1pct'] = dict(resets=float(nres[top].mean()), t0=float(nt0[top].mean()),
                                    bullets=float(nb[top].mean()), waves=float(nw[top].mean()))
         out['simd_all'] = dict(resets=float(nres.mean()), t0=float(nt0.mean()), bullets=float(nb.mean()))
+    rs = S[:, 16:20].astype(np.float64)
+    okr = (S[:, 9] > 0) & (S[:, 19] > 0)
+    if okr.any():   # inside the (last) reset pass of a wave: chain + LDS, draws, create, stores
+        r = S[okr]
+        out['reset_parts'] = dict(chain=float((r[:, 16] - r[:, 9]).mean()), draws=float((r[:, 17] - r[:, 16]).mean()),
+                                  create=float((r[:, 18] - r[:, 17]).mean()), stores=float((r[:, 19] - r[:, 18]).mean()),
+                                  after=float((r[:, 10] - r[:, 19]).mean()))
     out['slow10_reset_share'] = float(((Sm[:, 9] > 0) & (Sm[:, 10] > 0)).mean())
     print(json.dumps(out), flush=True)
     _lib._lib = None
@@ -215,6 +237,13 @@ def main():
             run(lib + ':c2', D._replace(reload_time=1000), 65536)
             run(lib + ':c3_noreset', D, 65536, auto_reset=False)
             stamps(lib + ':c3', D, 65536, lib=lib + '_stamps.so')
+        return
+    if a.set == 'c2':   # small-N layout study: c2 (4,096 envs, no bullets) and c3 for contrast
+        c2 = D._replace(reload_time=1000)
+        for k in ('quad', 'pair'):
+            stamps(k + '_c2_4k', c2, 4096, kernel=k)
+        stamps('quad_c2_4k_noreset', c2, 4096, kernel='quad', auto_reset=False)
+        stamps('pair_c3', D, 65536, kernel='pair')
         return
     if a.set == 'stamps_pair':
         stamps('pair_c3', D, 65536, kernel='pair')
