@@ -1702,12 +1702,19 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     int ctl = tick_control<S>(drv, i, sq, NN, kt);
     V pv[PPL];
     T mpx[PPL], mpy[PPL];
+    // 4 planet slots: read with the header, every slot (padding is masked
+    // below).  8 slots (config 5: 1-8 planets, 3.5 padded slots per env on
+    // average): read after the header, a slot past the env's planets
+    // aliased to slot 0 -- the line already read, no traffic -- one more
+    // round trip, which three waves per SIMD hide (c5: 56 B less per env,
+    // time unchanged in the A/B)
+    constexpr bool PLANETS_AFTER_HDR = PMAX > 4;
+    if constexpr (!PLANETS_AFTER_HDR) {
 #pragma unroll
-    for (int m = 0; m < PPL; ++m) {
-        const int j = q + LPE * m;
-        pv[m] = planets[size_t(j < p.p_pad ? j : 0) * NN + i];
-        mpx[m] = pv[m].x;
-        mpy[m] = pv[m].y;
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + LPE * m;
+            pv[m] = planets[size_t(j < p.p_pad ? j : 0) * NN + i];
+        }
     }
     const int tick = int(uint32_t(h.x) & TICK_MASK);
     const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
@@ -1716,6 +1723,18 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const int flags = (h.y >> 8) & 0xff;
     const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
     np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+    if constexpr (PLANETS_AFTER_HDR) {
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + LPE * m;
+            pv[m] = planets[size_t(j < np ? j : 0) * NN + i];
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) {
+        mpx[m] = pv[m].x;
+        mpy[m] = pv[m].y;
+    }
     // does any env of the wave use the last planet slot?  (uniform; with
     // planets_only < PMAX, e.g. the 3-planet games of config 3, none does
     // and the float64 fields skip that slot's division)

@@ -63,6 +63,22 @@ def main():
                    ratio=(2 * fetch + write) * 1024 / b['roofline']['bytes_per_launch'],
                    note='read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; memory-side counters, '
                         'Infinity Cache hits included')
+    rq = os.path.join(out, 'rdreq', 'run_counter_collection.csv')
+    wq = os.path.join(out, 'wrreq', 'run_counter_collection.csv')
+    if os.path.exists(rq) and os.path.exists(wq):
+        # memory-side requests by size: reads of 32, 64 or 128 B; a write
+        # request is 64 B (WRREQ_64B) or 32 B (the rest)
+        r, _ = counters(rq)
+        w2, _ = counters(wq)
+        g = lambda d, k: next((v for n, v in d.items() if n.startswith(k) and n[len(k):] in ('', '_sum')), 0.0)
+        n32, n64, n128 = g(r, 'TCC_EA0_RDREQ_32B'), g(r, 'TCC_EA0_RDREQ_64B'), g(r, 'TCC_EA0_RDREQ_128B')
+        nw, nw64 = g(w2, 'TCC_EA0_WRREQ'), g(w2, 'TCC_EA0_WRREQ_64B')
+        rd = 32 * n32 + 64 * n64 + 128 * n128
+        wr = 64 * nw64 + 32 * (nw - nw64)
+        traffic.update(rdreq=dict(total=g(r, 'TCC_EA0_RDREQ'), b32=n32, b64=n64, b128=n128),
+                       wrreq=dict(total=nw, b64=nw64),
+                       request_bytes_per_launch=rd + wr, request_read_bytes=rd, request_write_bytes=wr,
+                       request_ratio=(rd + wr) / b['roofline']['bytes_per_launch'])
     json.dump(traffic, open(os.path.join(out, 'traffic_%s_f32.json' % wl), 'w'), indent=1)
     i, ni = counters(os.path.join(out, 'insts', 'run_counter_collection.csv'))
     wv = i['SQ_WAVES']
