@@ -1,11 +1,19 @@
 set -u
 export TMPDIR=/tmp
-mkdir -p gpurun_out/s11
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/s11/full.log 2>&1 || { tail -40 gpurun_out/s11/full.log; exit 1; }
-tail -2 gpurun_out/s11/full.log
-timeout -k 10 300 python bench.py > gpurun_out/s11/bench_c3.log 2>&1 || exit 1
-for wl in c2 c5 c3any; do timeout -k 10 300 python bench.py --workload $wl --cpu-seconds 5 > gpurun_out/s11/bench_$wl.log 2>&1 || exit 1; done
-timeout -k 10 300 python bench.py --n-env 1048576 --no-cpu --steps 200 > gpurun_out/s11/bench_c3_1m.log 2>&1 || exit 1
-WL=c5 bash tools/profile_r2.sh || exit 1
-python tools/trace_outliers.py gpurun_out/r2prof/c5/stats/run_kernel_trace.csv > gpurun_out/r2prof/c5/outliers_c5.json
-for f in gpurun_out/s11/bench_*.log; do echo $f; grep metric $f | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step']*1e3, d['roofline']['frac'], d['stats']['mean_live_bullets'], d['stats']['resets_per_step'], d.get('rollout',{}).get('ms_per_tick',0)*1e3, d.get('cpu_baseline',{}).get('value'))"; done
+mkdir -p gpurun_out/s12
+L=libastro_hip_base,libastro_hip_skip,libastro_hip_pin
+for wl in c2 c3; do
+  timeout -k 10 300 python tools/ab.py --libs $L --workload $wl > gpurun_out/s12/ab_$wl.jsonl 2>&1 || exit 1
+done
+timeout -k 10 300 python tools/sweep.py --set c2 > gpurun_out/s12/stamps.jsonl 2>gpurun_out/s12/stamps.err || { tail gpurun_out/s12/stamps.err; exit 1; }
+cat gpurun_out/s12/ab_*.jsonl | grep -v amdgpu.ids | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['workload'], d['n'], d['lib'][12:] or 'main', round(d['us_per_launch_median'], 3), round(d['rollout_us_per_tick'], 3))
+"
+python3 -c "
+import json
+for l in open('gpurun_out/s12/stamps.jsonl'):
+    d=json.loads(l)
+    print(d['name'], {k:(round(v[0]) if isinstance(v,list) and v[0] else v) for k,v in d.items() if k in ('hdr_wait','loads2_sincos_gravity','ship_collide','bullets','reward','spawn_ships','planets','chain_hdr','reset')}, d['wave_end_us'])
+"
