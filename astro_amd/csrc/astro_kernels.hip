@@ -1404,6 +1404,9 @@ __device__ __forceinline__ bool quad_any(bool f, int lane) {
 #ifndef ASTRO_QUAD_WAVES
 #define ASTRO_QUAD_WAVES 4
 #endif
+#ifndef ASTRO_HELP_MAX_WAVES
+#define ASTRO_HELP_MAX_WAVES 2048
+#endif
 // Waves per quad-kernel workgroup.  The waves of a workgroup share nothing
 // (each has its own LDS rows and syncs only itself); four per workgroup make
 // a quarter as many workgroups for the dispatcher (launch floor 2.0 -> 1.6
@@ -1651,7 +1654,23 @@ struct QuadCounts {
 
 
 // One tick of the quad kernel's wave (16 envs), tick kt of the launch.
-template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false>
+// HELP: each step wave has a helper wave in its workgroup (waves QW..2QW-1)
+// that creates its finished games' next ones.  The step wave posts its
+// finished envs here as soon as it knows them -- before the surviving envs'
+// update -- and goes on; the helper, asleep until then, runs the reset
+// passes meanwhile, so a wave that has a finished game no longer ends a
+// reset pass (~3.9k cycles) after its physics.
+struct HelpBox {
+    uint32_t flag;                 // set (1) by the step wave once the rest is written
+    uint32_t pad;
+    unsigned long long todo;       // leader lanes (q == 0) of the finished envs
+    unsigned long long have_key;   // per lane: the pending key is known (key_valid or a key table)
+    int env[64];                   // per lane of the step wave: its env, pending seed and key
+    uint32_t seed[64];
+    uint32_t key[64];
+};
+
+template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false, bool HELP = false>
 __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
                                                 float *__restrict__ reward_all, uint8_t *__restrict__ done_all,
                                                 bool stats, int auto_reset, int kt STAMP_ARG) {
@@ -1664,7 +1683,10 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     __shared__ uint32_t s_index_all[QW][QWIN];           // a window of the wave's live bullets, see bw_*
     __shared__ int s_kept_all[QW][QENV], s_hit_all[QW][QENV], s_serial_all[QW][QENV];
     __shared__ uint32_t s_chain_all[QW][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
-    const int wv = QW == 1 ? 0 : int(threadIdx.x >> 6);
+    __shared__ HelpBox s_box_all[HELP ? QW : 1];
+    static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, several waves per workgroup");
+    const bool helper = HELP && int(threadIdx.x >> 6) >= QW;
+    const int wv = QW == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? QW : 0);   // (a helper: its step wave's)
     float4 (*s_body)[NBOD2] = s_body_all[wv];
     uint32_t *s_index = s_index_all[wv];
     int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv];
@@ -1679,6 +1701,42 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const bool active = base + e < N;     // uniform over the quad
     const int i = active ? base + e : N - 1;   // spare quads of the last wave shadow env N-1, store nothing
     const size_t NN = size_t(N);
+    if constexpr (HELP) {
+        // LDS holds the previous launch's leftovers: clear the flag before
+        // any step wave can post (every wave of the workgroup passes this
+        // one barrier; a wave past the last env returns after it, with its
+        // helper)
+        HelpBox &bx = s_box_all[wv];
+        if (helper && lane == 0) bx.flag = 0;
+        __syncthreads();
+        if (base >= N) return QuadCounts{};
+        if (helper) {
+            // until the step wave posts (bounded: it always posts, the bound
+            // only keeps a fault from hanging the device)
+            for (uint32_t spin = 0; *reinterpret_cast<volatile uint32_t *>(&bx.flag) == 0 && spin < (1u << 22); ++spin)
+                __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+            QuadCounts hc{};
+            const uint64_t todo0 = bx.todo;
+            if (todo0) {   // uniform
+                const int he = bx.env[lane];
+                const uint32_t hseed = bx.seed[lane], hkey = bx.key[lane];
+                const bool hk = (bx.have_key >> lane) & 1ull;
+                for (uint64_t todo = todo0; todo;)   // uniform
+                    todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, he, hseed, hkey, hk, s_chain,
+                                                            s_serial STAMP_PASS);
+                wave_sync();
+                if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
+                if (active && s_serial[e]) {   // uniform over the quad; rare
+                    const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(hkey)));
+                    const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[he];
+                    const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, c, stream_ring_of(st, he));
+                    restart_env<T, S, PMAX, LPE>(p, st, he, ng, q);
+                }
+            }
+            return hc;
+        }
+    }
     const size_t BC = size_t(p.b_cap);
     V *ships = reinterpret_cast<V *>(st.ships);
     T *ships_b = reinterpret_cast<T *>(st.ships_b);
@@ -2104,6 +2162,21 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         }
         if (q == 0) done_out[is] = done;
         STAMP(5);
+        if constexpr (HELP) {   // post the finished envs to the helper wave, then go on
+            // (lane 0 is active in every wave that gets here: base < N)
+            HelpBox &bx = s_box_all[wv];
+            const uint64_t todo = __ballot(done && auto_reset && q == 0);
+            if (todo) {   // uniform (the key of a first-step env may still be in flight: wait only here)
+                bx.env[lane] = is;
+                bx.seed[lane] = pend_seed;
+                bx.key[lane] = pend_key;
+                const uint64_t hk = __ballot(key_valid || p.key_table != nullptr);
+                if (lane == 0) bx.have_key = hk;
+            }
+            if (lane == 0) bx.todo = todo;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the box before the flag (LDS: in order per wave)
+            if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.flag) = 1u;
+        }
 
         if (!done) {   // uniform over the quad
             // ---- fire: ship s's bullet appended after the survivors, in ship order
@@ -2293,10 +2366,11 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // ---- auto-reset: the wave creates its finished envs' next games together,
     //      up to four per pass with 16 lanes each (wave_reset_pass); rejected
     //      randint words (max_planets not a power of two) take the serial path
+    if constexpr (!HELP)
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
         todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
                                            s_chain, s_serial STAMP_PASS);
-    if (auto_reset) {
+    if (!HELP && auto_reset) {
         wave_sync();
         if (stats) c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));
         if (active && s_serial[e]) {   // uniform over the quad; rare
@@ -2366,19 +2440,20 @@ struct QuadArgs {
 typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 
-template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false>
+template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false, bool HELP = false>
 #ifndef ASTRO_P8_WAVES
 #define ASTRO_P8_WAVES 3   // 8 planet slots: 141 VGPRs, no spills (4 waves: 128 VGPRs, 41 spilled; c5 34.3 -> 31.1 us)
 #endif
-__global__ __launch_bounds__(QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+__global__ __launch_bounds__(HELP ? 2 * QBLOCK : QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {
 #ifdef ASTRO_STAMPS
     unsigned long long stamp_[NSTAMP] = {};
-    quad_tick<T, S, PMAX, LPE>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0, stamp_);
+    quad_tick<T, S, PMAX, LPE, false, false, HELP>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0,
+                                                   stamp_);
     STAMP(11);
-    if (stats && (threadIdx.x & 63) == 0) {
+    if (stats && (threadIdx.x & 63) == 0 && int(threadIdx.x) < QBLOCK) {
         unsigned long long *row = stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * NSTAMP;
         for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
     }
@@ -2387,7 +2462,9 @@ __global__ __launch_bounds__(QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)
     //      grid-wide barrier between ticks (envs never interact); the
     //      counters go to the wave's stats row after every tick, so nothing
     //      but the tick number lives across the loop
-    if (int(blockIdx.x * QW + threadIdx.x / 64) * (64 / LPE) >= st.n_env) return;   // a spare wave of the last block
+    // (HELP: waves QW.. are the helpers of waves 0..QW-1, same stats row)
+    if (!HELP && int(blockIdx.x * QW + threadIdx.x / 64) * (64 / LPE) >= st.n_env) return;   // a spare wave of the last block
+    // (HELP: a spare wave returns inside quad_tick, after the workgroup's one barrier)
     const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
     for (int kt = 0; kt < n_ticks; ++kt) {
         QuadCounts c;
@@ -2401,11 +2478,14 @@ __global__ __launch_bounds__(QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)
             c = quad_tick<T, S, PMAX, LPE, true, BOTS>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr,
                                                         a.auto_reset, kt);
         } else {
-            c = quad_tick<T, S, PMAX, LPE>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, kt);
+            c = quad_tick<T, S, PMAX, LPE, false, false, HELP>(p, st, drv, reward_all, done_all, stats != nullptr,
+                                                               auto_reset, kt);
         }
-        if (stats)
-            flush_counts(stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * ASTRO_NSTATS, c,
-                         p.b_cap * (64 / LPE) < 65536);
+        if (stats) {
+            const int row = __builtin_amdgcn_readfirstlane(int(blockIdx.x * QW + (threadIdx.x / 64) % QW));
+            if (row * (64 / LPE) < st.n_env)
+                flush_counts(stats + size_t(row) * ASTRO_NSTATS, c, p.b_cap * (64 / LPE) < 65536);
+        }
         // this tick's stores (other lanes' bullets included) before the
         // wave's next tick reads them: vmcnt(0), on this CU's own L1
         if (kt + 1 < n_ticks) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -2687,6 +2767,17 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 2, true>), dim3(g2), dim3(QBLOCK), 0, stream,
                                p, s, drv, r, d, st, ar);
             return launched("astro_step(pair, bots)");
+        }
+        // a one-tick launch of at most ASTRO_HELP_MAX_WAVES waves (two per
+        // SIMD: c2, c3) gets helper waves for its resets (HelpBox)
+        if (one && ar && int64_t(s.n_env) * lpe <= int64_t(64) * ASTRO_HELP_MAX_WAVES) {
+            if (lpe == 4)
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, true>), dim3(grid),
+                                   dim3(2 * QBLOCK), 0, stream, p, s, drv, r, d, st, ar);
+            else
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true>), dim3(grid),
+                                   dim3(2 * QBLOCK), 0, stream, p, s, drv, r, d, st, ar);
+            return launched(lpe == 4 ? "astro_step(quad, helpers)" : "astro_step(pair, helpers)");
         }
         if (lpe == 4 && one)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,

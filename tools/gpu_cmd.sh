@@ -1,19 +1,17 @@
 set -u
 export TMPDIR=/tmp
-mkdir -p gpurun_out/s12
-L=libastro_hip_base,libastro_hip_skip,libastro_hip_pin
+mkdir -p gpurun_out/s13
+L=libastro_hip_nohelp,libastro_hip
 for wl in c2 c3; do
-  timeout -k 10 300 python tools/ab.py --libs $L --workload $wl > gpurun_out/s12/ab_$wl.jsonl 2>&1 || exit 1
+  timeout -k 10 120 python tools/ab.py --libs $L --workload $wl > gpurun_out/s13/ab_$wl.jsonl 2>&1 || { tail -5 gpurun_out/s13/ab_$wl.jsonl; exit 1; }
 done
-timeout -k 10 300 python tools/sweep.py --set c2 > gpurun_out/s12/stamps.jsonl 2>gpurun_out/s12/stamps.err || { tail gpurun_out/s12/stamps.err; exit 1; }
-cat gpurun_out/s12/ab_*.jsonl | grep -v amdgpu.ids | python3 -c "
+cat gpurun_out/s13/ab_*.jsonl | grep -v amdgpu.ids | python3 -c "
 import sys, json
 for l in sys.stdin:
     d = json.loads(l); print(d['workload'], d['n'], d['lib'][12:] or 'main', round(d['us_per_launch_median'], 3), round(d['rollout_us_per_tick'], 3))
 "
-python3 -c "
-import json
-for l in open('gpurun_out/s12/stamps.jsonl'):
-    d=json.loads(l)
-    print(d['name'], {k:(round(v[0]) if isinstance(v,list) and v[0] else v) for k,v in d.items() if k in ('hdr_wait','loads2_sincos_gravity','ship_collide','bullets','reward','spawn_ships','planets','chain_hdr','reset')}, d['wave_end_us'])
-"
+timeout -k 10 120 python bench.py --workload c2 --no-cpu > gpurun_out/s13/bench_c2.log 2>&1 || exit 1
+timeout -k 10 120 python bench.py --no-cpu > gpurun_out/s13/bench_c3.log 2>&1 || exit 1
+for f in gpurun_out/s13/bench_*.log; do grep metric $f | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$f', d['ms_per_step']*1e3, d['stats']['resets_per_step'], d['stats']['serial_resets_per_step'])"; done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/s13/full.log 2>&1 || { tail -40 gpurun_out/s13/full.log; exit 1; }
+tail -2 gpurun_out/s13/full.log
