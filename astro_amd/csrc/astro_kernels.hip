@@ -747,7 +747,7 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
             stamp_[k == 0 ? 12 : 13] = t_;                                                \
         }                                                                                \
     } while (0)
-constexpr int NSTAMP = 24;   // 0-13 step sections, 14-15 placement, 16-19 reset pass
+constexpr int NSTAMP = 24;   // 0-13 step sections, 14-15 placement, 16-19 reset pass, 20-22 helper wave
 #else
 #define STAMP(k) \
     do {         \
@@ -1404,6 +1404,12 @@ __device__ __forceinline__ bool quad_any(bool f, int lane) {
 #ifndef ASTRO_QUAD_WAVES
 #define ASTRO_QUAD_WAVES 4
 #endif
+// waves per workgroup of the small-N (quad) helper instance: config 2's 256
+// waves on 128 CUs, not 64 (c2 6.18 -> 5.52 us A/B; c3 wants four)
+#ifndef ASTRO_QW_SMALL
+#define ASTRO_QW_SMALL 2
+#endif
+constexpr int QW_SMALL = ASTRO_QW_SMALL;
 #ifndef ASTRO_HELP_MAX_WAVES
 #define ASTRO_HELP_MAX_WAVES 2048
 #endif
@@ -1670,7 +1676,23 @@ struct HelpBox {
     uint32_t key[64];
 };
 
-template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false, bool HELP = false>
+// Post a step wave's finished envs (leader lanes `todo`) to its helper.
+__device__ __forceinline__ void help_post(HelpBox &bx, uint64_t todo, int lane, int env, uint32_t seed, uint32_t key,
+                                          bool have_key) {
+    if (todo) {   // uniform (the key of a first-step env may still be in flight: wait only here)
+        bx.env[lane] = env;
+        bx.seed[lane] = seed;
+        bx.key[lane] = key;
+        const uint64_t hk = __ballot(have_key);
+        if (lane == 0) bx.have_key = hk;
+    }
+    if (lane == 0) bx.todo = todo;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the box before the flag (LDS: in order per wave)
+    if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.flag) = 1u;
+}
+
+template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false, bool HELP = false,
+          int WPG = QW>
 __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
                                                 float *__restrict__ reward_all, uint8_t *__restrict__ done_all,
                                                 bool stats, int auto_reset, int kt STAMP_ARG) {
@@ -1679,14 +1701,14 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     constexpr int QENV = 64 / LPE;    // envs per wave
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
     // LDS, one set per wave of the workgroup
-    __shared__ float4 s_body_all[QW][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
-    __shared__ uint32_t s_index_all[QW][QWIN];           // a window of the wave's live bullets, see bw_*
-    __shared__ int s_kept_all[QW][QENV], s_hit_all[QW][QENV], s_serial_all[QW][QENV];
-    __shared__ uint32_t s_chain_all[QW][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
-    __shared__ HelpBox s_box_all[HELP ? QW : 1];
-    static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, several waves per workgroup");
-    const bool helper = HELP && int(threadIdx.x >> 6) >= QW;
-    const int wv = QW == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? QW : 0);   // (a helper: its step wave's)
+    __shared__ float4 s_body_all[WPG][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
+    __shared__ uint32_t s_index_all[WPG][QWIN];           // a window of the wave's live bullets, see bw_*
+    __shared__ int s_kept_all[WPG][QENV], s_hit_all[WPG][QENV], s_serial_all[WPG][QENV];
+    __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
+    __shared__ HelpBox s_box_all[HELP ? WPG : 1];
+    static_assert(!HELP || (WPG > 1 && !OPAQUE), "helper waves: one-tick launches, several waves per workgroup");
+    const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
+    const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
     float4 (*s_body)[NBOD2] = s_body_all[wv];
     uint32_t *s_index = s_index_all[wv];
     int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv];
@@ -1697,7 +1719,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     if constexpr (OPAQUE) asm volatile("" : "+v"(lane));   // (see the rollout kernel)
     const int q = lane & (LPE - 1);
     const int e = lane / LPE;
-    const int base = (blockIdx.x * QW + wv) * QENV;
+    const int base = (blockIdx.x * WPG + wv) * QENV;
     const bool active = base + e < N;     // uniform over the quad
     const int i = active ? base + e : N - 1;   // spare quads of the last wave shadow env N-1, store nothing
     const size_t NN = size_t(N);
@@ -1716,6 +1738,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             for (uint32_t spin = 0; *reinterpret_cast<volatile uint32_t *>(&bx.flag) == 0 && spin < (1u << 22); ++spin)
                 __builtin_amdgcn_s_sleep(1);
             asm volatile("" ::: "memory");
+#ifdef ASTRO_STAMPS
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[20])::"memory");
+#endif
             QuadCounts hc{};
             const uint64_t todo0 = bx.todo;
             if (todo0) {   // uniform
@@ -1734,6 +1759,10 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                     restart_env<T, S, PMAX, LPE>(p, st, he, ng, q);
                 }
             }
+#ifdef ASTRO_STAMPS
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[21])::"memory");
+            stamp_[22] = __popcll(todo0);
+#endif
             return hc;
         }
     }
@@ -1954,6 +1983,21 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     }
     wave_sync();
 
+    // (quad instance only: in the pair instance the extra live range spills)
+    constexpr bool EARLY_POST = HELP && LPE == 4;
+    if constexpr (EARLY_POST) {
+        // a wave without live bullets (every wave of config 2) knows its
+        // finished envs now -- a ship collision or the timeout -- so it
+        // posts them before its bullet pass and output section, not after
+        if (total == 0) {   // uniform
+            bool fin = !live;
+#pragma unroll
+            for (int s = 0; s < S; ++s) fin |= quad_any<LPE>(hsp[s], lane);
+            help_post(s_box_all[wv], __ballot(active && fin && auto_reset && q == 0), lane, i, pend_seed, pend_key,
+                      key_valid || p.key_table != nullptr);
+        }
+    }
+
     STAMP(3);
     // ---- bullets (core.py:241-251, 264-266, 295-300): lane g of a round
     //      takes live bullet r0 + g of the wave: collide with the OLD bodies,
@@ -2164,18 +2208,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         STAMP(5);
         if constexpr (HELP) {   // post the finished envs to the helper wave, then go on
             // (lane 0 is active in every wave that gets here: base < N)
-            HelpBox &bx = s_box_all[wv];
-            const uint64_t todo = __ballot(done && auto_reset && q == 0);
-            if (todo) {   // uniform (the key of a first-step env may still be in flight: wait only here)
-                bx.env[lane] = is;
-                bx.seed[lane] = pend_seed;
-                bx.key[lane] = pend_key;
-                const uint64_t hk = __ballot(key_valid || p.key_table != nullptr);
-                if (lane == 0) bx.have_key = hk;
-            }
-            if (lane == 0) bx.todo = todo;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the box before the flag (LDS: in order per wave)
-            if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.flag) = 1u;
+            if (!EARLY_POST || total > 0)   // uniform (a wave without bullets posted before its bullet pass)
+                help_post(s_box_all[wv], __ballot(done && auto_reset && q == 0), lane, is, pend_seed, pend_key,
+                          key_valid || p.key_table != nullptr);
         }
 
         if (!done) {   // uniform over the quad
@@ -2440,30 +2475,32 @@ struct QuadArgs {
 typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 
-template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false, bool HELP = false>
+template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false, bool HELP = false,
+          int WPG = QW>
 #ifndef ASTRO_P8_WAVES
 #define ASTRO_P8_WAVES 3   // 8 planet slots: 141 VGPRs, no spills (4 waves: 128 VGPRs, 41 spilled; c5 34.3 -> 31.1 us)
 #endif
-__global__ __launch_bounds__(HELP ? 2 * QBLOCK : QBLOCK, MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+__global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {
 #ifdef ASTRO_STAMPS
     unsigned long long stamp_[NSTAMP] = {};
-    quad_tick<T, S, PMAX, LPE, false, false, HELP>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0,
+    quad_tick<T, S, PMAX, LPE, false, false, HELP, WPG>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0,
                                                    stamp_);
     STAMP(11);
-    if (stats && (threadIdx.x & 63) == 0 && int(threadIdx.x) < QBLOCK) {
-        unsigned long long *row = stats + size_t(blockIdx.x * QW + threadIdx.x / 64) * NSTAMP;
-        for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
+    if (stats && (threadIdx.x & 63) == 0) {   // a helper wave: slots 20-22 of its step wave's row
+        const bool hw = int(threadIdx.x) >= (64 * WPG);
+        unsigned long long *row = stats + size_t(blockIdx.x * WPG + (threadIdx.x / 64) % WPG) * NSTAMP;
+        for (int k = hw ? 20 : 0; k < (hw ? 23 : 20); ++k) row[k] = stamp_[k];
     }
 #else
     // ---- the launch's ticks: each wave steps its 16 envs on its own, no
     //      grid-wide barrier between ticks (envs never interact); the
     //      counters go to the wave's stats row after every tick, so nothing
     //      but the tick number lives across the loop
-    // (HELP: waves QW.. are the helpers of waves 0..QW-1, same stats row)
-    if (!HELP && int(blockIdx.x * QW + threadIdx.x / 64) * (64 / LPE) >= st.n_env) return;   // a spare wave of the last block
+    // (HELP: waves WPG.. are the helpers of waves 0..WPG-1, same stats row)
+    if (!HELP && int(blockIdx.x * WPG + threadIdx.x / 64) * (64 / LPE) >= st.n_env) return;   // a spare wave of the last block
     // (HELP: a spare wave returns inside quad_tick, after the workgroup's one barrier)
     const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
     for (int kt = 0; kt < n_ticks; ++kt) {
@@ -2478,11 +2515,11 @@ __global__ __launch_bounds__(HELP ? 2 * QBLOCK : QBLOCK, MULTI ? 2 : (PMAX > 4 ?
             c = quad_tick<T, S, PMAX, LPE, true, BOTS>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr,
                                                         a.auto_reset, kt);
         } else {
-            c = quad_tick<T, S, PMAX, LPE, false, false, HELP>(p, st, drv, reward_all, done_all, stats != nullptr,
+            c = quad_tick<T, S, PMAX, LPE, false, false, HELP, WPG>(p, st, drv, reward_all, done_all, stats != nullptr,
                                                                auto_reset, kt);
         }
         if (stats) {
-            const int row = __builtin_amdgcn_readfirstlane(int(blockIdx.x * QW + (threadIdx.x / 64) % QW));
+            const int row = __builtin_amdgcn_readfirstlane(int(blockIdx.x * WPG + (threadIdx.x / 64) % WPG));
             if (row * (64 / LPE) < st.n_env)
                 flush_counts(stats + size_t(row) * ASTRO_NSTATS, c, p.b_cap * (64 / LPE) < 65536);
         }
@@ -2771,9 +2808,10 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         // a one-tick launch of at most ASTRO_HELP_MAX_WAVES waves (two per
         // SIMD: c2, c3) gets helper waves for its resets (HelpBox)
         if (one && ar && int64_t(s.n_env) * lpe <= int64_t(64) * ASTRO_HELP_MAX_WAVES) {
-            if (lpe == 4)
-                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, true>), dim3(grid),
-                                   dim3(2 * QBLOCK), 0, stream, p, s, drv, r, d, st, ar);
+            if (lpe == 4)   // (small N: two step waves per workgroup spread the few waves over more CUs)
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, true, QW_SMALL>),
+                                   dim3(int((int64_t(s.n_env) * 4 + 64 * QW_SMALL - 1) / (64 * QW_SMALL))),
+                                   dim3(2 * 64 * QW_SMALL), 0, stream, p, s, drv, r, d, st, ar);
             else
                 hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true>), dim3(grid),
                                    dim3(2 * QBLOCK), 0, stream, p, s, drv, r, d, st, ar);

@@ -111,6 +111,18 @@ def stamps(name, cfg, n, ticks=20, warm=150, b_cap=32, p_pad=4, lib='libastro_hi
     out['wave_start_us'] = dict(mean=float(st_rel.mean()), p90=float(np.percentile(st_rel, 90)), max=float(st_rel.max()))
     out['wave_end_us'] = dict(mean=float(en_rel.mean()), p90=float(np.percentile(en_rel, 90)),
                               launch_mean=float(np.mean([e.max() for e in np.split(en_rel, ticks)])))
+    if (S[:, 21] > 0).any():   # helper waves (HelpBox): posted -> done, relative to the launch's first wave
+        hs, he = [], []
+        for t in range(ticks):
+            sl = slice(t * rows_per, (t + 1) * rows_per)
+            t0w = S[sl, 12].min()
+            ok = S[sl, 21] > 0
+            hs.append((S[sl, 20][ok] - t0w) / 100.0)
+            he.append((S[sl, 21][ok] - t0w) / 100.0)
+        ends = [x.max() for x in he if x.size]
+        out['helper_us'] = dict(seen_mean=float(np.concatenate(hs).mean()), end_mean=float(np.concatenate(he).mean()),
+                                end_launch_mean=float(np.mean(ends)) if ends else None,
+                                busy_frac=float((S[:, 22] > 0).mean()))
     if ncr:
         t0 = R[:, :nw, 12].min(1)[:, None].astype(np.float64)
         cs, cl, ce = [(C[:, :, k] - t0) / 100.0 for k in (0, 1, 2)]
