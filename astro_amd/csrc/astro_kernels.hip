@@ -1558,11 +1558,12 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
 // then runs spread over the row (ship u, planet u).  An env whose first
 // randint word is rejected is flagged in s_serial for the quad's serial
 // create.  Returns the leaders not yet served.
-template <typename T, int S, int PMAX, int LPE>
+template <typename T, int S, int PMAX, int LPE, bool PRE = false>
 __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
                                                     int lane, int i, uint32_t pend_seed, uint32_t pend_key,
                                                     bool have_key, uint32_t (*s_chain)[2][13 + 2 * S],
-                                                    int *s_serial STAMP_ARG) {
+                                                    int *s_serial STAMP_ARG,
+                                                    const uint32_t (*pre)[2][13 + 2 * S] = nullptr) {
     constexpr int NW = 12 + 2 * S;   // outputs create() draws, randint accepting its first word
     int leader[4];
 #pragma unroll
@@ -1580,22 +1581,32 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     const bool hk = __shfl(int(have_key), src, 64) != 0;
     const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[ie];   // used last: in flight meanwhile
 
-    // init-key chains: even lanes run key[0..] from the seed, odd lanes key[397..]
-    const uint32_t k397 = hk ? key : mt_key_at(seed, 0, MT_PROLOGUE);
-    const bool bchain = u & 1;
-    const uint32_t koff = bchain ? 397u : 0u;
-    uint32_t xs[NW + 1];
-    xs[0] = bchain ? k397 : seed;
-#pragma unroll
-    for (int k = 0; k < NW; ++k) xs[k + 1] = mt_key_next(xs[k], koff + uint32_t(k + 1));
-    if (u < 2) {
-#pragma unroll
-        for (int k = 0; k <= NW; ++k) s_chain[row][u][k] = xs[k];
-    }
-    wave_sync();
     const int uw = u < NW ? u : 0;
-    const uint32_t a0 = s_chain[row][0][uw], a1 = s_chain[row][0][uw + 1], b0 = s_chain[row][1][uw];
-    wave_sync();   // s_chain is free for the next pass
+    uint32_t a0, a1, b0;
+    if constexpr (PRE) {   // the env's two chains, made ahead (a helper wave, HelpBox)
+        const int le = src / LPE;
+        a0 = pre[le][0][uw];
+        a1 = pre[le][0][uw + 1];
+        b0 = pre[le][1][uw];
+    } else {
+        // init-key chains: even lanes run key[0..] from the seed, odd lanes key[397..]
+        const uint32_t k397 = hk ? key : mt_key_at(seed, 0, MT_PROLOGUE);
+        const bool bchain = u & 1;
+        const uint32_t koff = bchain ? 397u : 0u;
+        uint32_t xs[NW + 1];
+        xs[0] = bchain ? k397 : seed;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) xs[k + 1] = mt_key_next(xs[k], koff + uint32_t(k + 1));
+        if (u < 2) {
+#pragma unroll
+            for (int k = 0; k <= NW; ++k) s_chain[row][u][k] = xs[k];
+        }
+        wave_sync();
+        a0 = s_chain[row][0][uw];
+        a1 = s_chain[row][0][uw + 1];
+        b0 = s_chain[row][1][uw];
+        wave_sync();   // s_chain is free for the next pass
+    }
     const uint32_t y = (a0 & 0x80000000u) | (a1 & 0x7fffffffu);
     const uint32_t w = mt_temper(b0 ^ (y >> 1) ^ ((a1 & 1u) ? 0x9908b0dfu : 0u));   // output u
     STAMP(16);
@@ -1667,27 +1678,15 @@ struct QuadCounts {
 // passes meanwhile, so a wave that has a finished game no longer ends a
 // reset pass (~3.9k cycles) after its physics.
 struct HelpBox {
-    uint32_t flag;                 // set (1) by the step wave once the rest is written
+    uint32_t flag;                 // set (1) by the step wave once `todo` is written
     uint32_t pad;
     unsigned long long todo;       // leader lanes (q == 0) of the finished envs
-    unsigned long long have_key;   // per lane: the pending key is known (key_valid or a key table)
-    int env[64];                   // per lane of the step wave: its env, pending seed and key
-    uint32_t seed[64];
-    uint32_t key[64];
 };
 
 // Post a step wave's finished envs (leader lanes `todo`) to its helper.
-__device__ __forceinline__ void help_post(HelpBox &bx, uint64_t todo, int lane, int env, uint32_t seed, uint32_t key,
-                                          bool have_key) {
-    if (todo) {   // uniform (the key of a first-step env may still be in flight: wait only here)
-        bx.env[lane] = env;
-        bx.seed[lane] = seed;
-        bx.key[lane] = key;
-        const uint64_t hk = __ballot(have_key);
-        if (lane == 0) bx.have_key = hk;
-    }
+__device__ __forceinline__ void help_post(HelpBox &bx, uint64_t todo, int lane) {
     if (lane == 0) bx.todo = todo;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the box before the flag (LDS: in order per wave)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the mask before the flag (LDS: in order per wave)
     if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.flag) = 1u;
 }
 
@@ -1706,6 +1705,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     __shared__ int s_kept_all[WPG][QENV], s_hit_all[WPG][QENV], s_serial_all[WPG][QENV];
     __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
     __shared__ HelpBox s_box_all[HELP ? WPG : 1];
+    __shared__ uint32_t s_pre_all[HELP ? WPG : 1][HELP ? QENV : 1][2][13 + 2 * S];   // a helper's chains, made ahead
     static_assert(!HELP || (WPG > 1 && !OPAQUE), "helper waves: one-tick launches, several waves per workgroup");
     const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
     const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
@@ -1733,6 +1733,31 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         __syncthreads();
         if (base >= N) return QuadCounts{};
         if (helper) {
+            // While its step wave steps, the helper makes the MT19937 init-key
+            // chains of every env's pending game (the first 13 + 2S words from
+            // the seed and from key[397]; 2 lanes per env, all envs at once):
+            // a reset pass then starts from its draws.  A finished env's
+            // header is never written by its step wave, so the helper reads
+            // the same pending seed and key (the step wave's gather of a
+            // first-step env's key repeated here).
+            constexpr int NW = 12 + 2 * S;
+            uint32_t (*pre)[2][13 + 2 * S] = s_pre_all[wv];
+            const int4 hh = reinterpret_cast<const int4 *>(st.hdr)[i];
+            const uint32_t hseed = uint32_t(hh.z);
+            const bool kvalid = (uint32_t(hh.x) & KEY_VALID) != 0;
+            uint32_t hkey = uint32_t(hh.w);
+            const bool hk = kvalid || p.key_table != nullptr;
+            if (q == 1 && !kvalid) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
+            if (q < 2) {
+                uint32_t x = q == 0 ? hseed : hkey;
+                const uint32_t koff = q == 0 ? 0u : 397u;
+#pragma unroll
+                for (int k = 0; k <= NW; ++k) {
+                    pre[e][q][k] = x;
+                    x = mt_key_next(x, koff + uint32_t(k + 1));
+                }
+            }
+            wave_sync();
             // until the step wave posts (bounded: it always posts, the bound
             // only keeps a fault from hanging the device)
             for (uint32_t spin = 0; *reinterpret_cast<volatile uint32_t *>(&bx.flag) == 0 && spin < (1u << 22); ++spin)
@@ -1744,19 +1769,16 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             QuadCounts hc{};
             const uint64_t todo0 = bx.todo;
             if (todo0) {   // uniform
-                const int he = bx.env[lane];
-                const uint32_t hseed = bx.seed[lane], hkey = bx.key[lane];
-                const bool hk = (bx.have_key >> lane) & 1ull;
                 for (uint64_t todo = todo0; todo;)   // uniform
-                    todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, he, hseed, hkey, hk, s_chain,
-                                                            s_serial STAMP_PASS);
+                    todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, s_chain,
+                                                                  s_serial STAMP_PASS, pre);
                 wave_sync();
                 if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
                 if (active && s_serial[e]) {   // uniform over the quad; rare
-                    const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(hkey)));
-                    const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[he];
-                    const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, c, stream_ring_of(st, he));
-                    restart_env<T, S, PMAX, LPE>(p, st, he, ng, q);
+                    const uint32_t kq = uint32_t(quad_bcast_i<1, LPE>(int(hkey)));   // (lane q == 1 has the key)
+                    const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+                    const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, c, stream_ring_of(st, i));
+                    restart_env<T, S, PMAX, LPE>(p, st, i, ng, q);
                 }
             }
 #ifdef ASTRO_STAMPS
@@ -1993,8 +2015,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             bool fin = !live;
 #pragma unroll
             for (int s = 0; s < S; ++s) fin |= quad_any<LPE>(hsp[s], lane);
-            help_post(s_box_all[wv], __ballot(active && fin && auto_reset && q == 0), lane, i, pend_seed, pend_key,
-                      key_valid || p.key_table != nullptr);
+            help_post(s_box_all[wv], __ballot(active && fin && auto_reset && q == 0), lane);
         }
     }
 
@@ -2209,8 +2230,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         if constexpr (HELP) {   // post the finished envs to the helper wave, then go on
             // (lane 0 is active in every wave that gets here: base < N)
             if (!EARLY_POST || total > 0)   // uniform (a wave without bullets posted before its bullet pass)
-                help_post(s_box_all[wv], __ballot(done && auto_reset && q == 0), lane, is, pend_seed, pend_key,
-                          key_valid || p.key_table != nullptr);
+                help_post(s_box_all[wv], __ballot(done && auto_reset && q == 0), lane);
         }
 
         if (!done) {   // uniform over the quad
