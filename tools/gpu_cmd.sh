@@ -1,20 +1,12 @@
 set -u
 export TMPDIR=/tmp
-mkdir -p gpurun_out/s20
-L=libastro_hip_h1,libastro_hip
+mkdir -p gpurun_out/s21
+L=libastro_hip_h3,libastro_hip_h4
 for wl in c3 c2; do
-  timeout -k 10 200 python tools/ab.py --libs $L --workload $wl > gpurun_out/s20/ab_$wl.jsonl 2>&1 || { tail -5 gpurun_out/s20/ab_$wl.jsonl; exit 1; }
+  timeout -k 10 200 python tools/ab.py --libs $L --workload $wl > gpurun_out/s21/ab_$wl.jsonl 2>&1 || { tail -5 gpurun_out/s21/ab_$wl.jsonl; exit 1; }
 done
-cat gpurun_out/s20/ab_*.jsonl | grep -v amdgpu.ids | python3 -c "
+cat gpurun_out/s21/ab_*.jsonl | grep -v amdgpu.ids | python3 -c "
 import sys, json
 for l in sys.stdin:
     d = json.loads(l); print(d['workload'], d['n'], d['lib'][12:] or 'main', round(d['us_per_launch_median'], 3), round(d['rollout_us_per_tick'], 3))
-"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/s20/full.log 2>&1 || { tail -40 gpurun_out/s20/full.log; exit 1; }
-tail -2 gpurun_out/s20/full.log
-timeout -k 10 300 python tools/sweep.py --set c2 > gpurun_out/s20/stamps.jsonl 2>gpurun_out/s20/stamps.err || { tail gpurun_out/s20/stamps.err; exit 1; }
-python3 -c "
-import json
-for l in open('gpurun_out/s20/stamps.jsonl'):
-    d=json.loads(l); print(d['name'], d['wave_end_us'], d.get('helper_us'))
 "
