@@ -381,7 +381,10 @@ def test_config4_eight_shards_compose():
     """BASELINE.json config 4's sharding on one GPU: 8 BatchedEnv shards of
     65,536 envs (env_offset = rank * 65,536, as bench.py's ranks) stepped
     200 ticks equal one 524,288-env run bit for bit -- headers, stream
-    cursors and rings, ships, planets, bullets."""
+    cursors and rings, ships, planets, bullets.  (The shards' launches, two
+    step waves per SIMD, create their finished games' next ones on helper
+    waves -- HelpBox in the kernel -- the full run's step waves create their
+    own: the two paths must agree.)"""
     cfg = CFG['default']
     n, G, ticks = 65536, 8, 200
     from astro_amd import BatchedEnv
