@@ -1410,6 +1410,12 @@ __device__ __forceinline__ bool quad_any(bool f, int lane) {
 #define ASTRO_QW_SMALL 2
 #endif
 constexpr int QW_SMALL = ASTRO_QW_SMALL;
+#ifndef ASTRO_QW_PAIR_HELP
+#define ASTRO_QW_PAIR_HELP 8
+#endif
+// step waves per workgroup of the pair instance with helpers (c3: eight,
+// 16-wave workgroups, 12.55 -> 12.13 us A/B; two: 13.12)
+constexpr int QW_PAIR_HELP = ASTRO_QW_PAIR_HELP;
 #ifndef ASTRO_HELP_MAX_WAVES
 #define ASTRO_HELP_MAX_WAVES 2048
 #endif
@@ -1671,6 +1677,135 @@ struct QuadCounts {
 
 
 // One tick of the quad kernel's wave (16 envs), tick kt of the launch.
+// The surviving envs' planet update (core.py:289-294): gravity of all
+// planets incl. self, in the reference's order; float32 at tick 0 / for a
+// lone planet.  Lane q's planet slots q + LPE m -> out[m] (slots < np);
+// every lane of a group calls it (DPP broadcasts).  The step wave runs it
+// for its surviving envs, or -- with helper waves -- the helper runs it for
+// every env during the step and stores the survivors' after the post.
+template <typename T, int S, int PMAX, int LPE, int PPL>
+__device__ __forceinline__ void planet_update(const AstroParams &p, const typename Store<T>::V (&pv)[PPL],
+                                              const T (&mpx)[PPL], const T (&mpy)[PPL], int q, int np, bool t0,
+                                              bool slot_last, typename Store<T>::V (&out)[PPL]) {
+    using V = typename Store<T>::V;
+    const float dtf = float(p.dt);
+    double px[PMAX], py[PMAX];
+    {   // the planets again from the quad (DPP) rather than 2*PMAX
+        // doubles held live across the bullet pass
+        T rx[PPL], ry[PPL];
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            rx[m] = mpx[m];
+            ry[m] = mpy[m];
+            asm volatile("" : "+v"(rx[m]), "+v"(ry[m]));
+        }
+        bcast_slots<T, PPL, LPE>(rx, px);
+        bcast_slots<T, PPL, LPE>(ry, py);
+    }
+    // Pair kernel, 4 slots: the float64 planet-planet factors
+    // gm / max(1e-12, d2) of the 6 distinct pairs, 3 per lane (d2 and
+    // so the factor are the same bit for bit both ways round), the
+    // partner's two by DPP; row i of lane q's planets i = q, q + 2 is
+    // then F(i, j) for j = 0..3 (see symmetric_rows)
+    double Fr[PPL][PMAX];
+    if constexpr (LPE == 2 && PMAX == 4) {
+        const bool l0 = q == 0;
+        // F(i, j) on lane 0, F(i1, j1) on lane 1: operands selected
+        // first, one division per lane
+        // (both lanes' differences, then one selected: a select between the
+        // array elements would index the arrays in memory)
+        auto fac = [&](int i, int j, int i1, int j1) {
+            const double dx0 = px[j] - px[i], dx1 = px[j1] - px[i1];
+            const double dy0 = py[j] - py[i], dy1 = py[j1] - py[i1];
+            const double ddx = l0 ? dx0 : dx1, ddy = l0 ? dy0 : dy1;
+            return div_gravity(p.gm, max_floor(ddx * ddx + ddy * ddy));
+        };
+        // lane 0: A = F01, B = F03, C = F02; lane 1: A = F12, B = F23, C = F13
+        // (B is only read for planet slot 3: skipped when no env has it)
+        const double A = fac(0, 1, 1, 2);
+        const double B = slot_last ? fac(0, 3, 2, 3) : 0.0;
+        const double C = fac(0, 2, 1, 3);
+        const double A2 = pair_swap(A), B2 = pair_swap(B);   // lane 0: F12, F23; lane 1: F01, F03
+        const double z = 0.0;   // (self: unused)
+        // planet q:     lane 0 [-, F01, F02, F03]   lane 1 [F10, -, F12, F13]
+        // planet q + 2: lane 0 [F20, F21, -, F23]   lane 1 [F30, F31, F32, -]
+        Fr[0][0] = l0 ? z : A2;
+        Fr[0][1] = l0 ? A : z;
+        Fr[0][2] = l0 ? C : A;
+        Fr[0][3] = l0 ? B : C;
+        Fr[1][0] = l0 ? C : B2;
+        Fr[1][1] = l0 ? A2 : C;
+        Fr[1][2] = l0 ? z : B;
+        Fr[1][3] = l0 ? B2 : z;
+    }
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) {
+        const int j = q + LPE * m;
+        if (j < np) {
+            const double pxj = double(mpx[m]), pyj = double(mpy[m]);
+            const double pdx = double(pv[m].z), pdy = double(pv[m].w);
+            V v;
+            if (np == 1) {
+                // a lone planet's own field: r = +0, so gm / max(1e-12, 0) * r
+                // is a zero with the sign of gm, exactly
+                const float g0 = p.gm < 0.0 ? -0.0f : 0.0f;
+                const float ndx = float(pdx) + g0 * dtf, ndy = float(pdy) + g0 * dtf;
+                v.x = T(wrap_unit<float>(float(pxj) + dtf * ndx));
+                v.y = T(wrap_unit<float>(float(pyj) + dtf * ndy));
+                v.z = T(ndx);
+                v.w = T(ndy);
+            } else {
+                double ndx, ndy;
+                if (t0) {
+                    float gx, gy;
+                    field<float, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
+                    ndx = pdx + double(gx * dtf);
+                    ndy = pdy + double(gy * dtf);
+                } else {
+                    double gx, gy;
+#ifdef ASTRO_ABLATE_PLANETFIELD   // timing ablation only (wrong results)
+                    gx = px[1] - pxj;
+                    gy = py[1] - pyj;
+#else
+                    if constexpr (LPE == 2 && PMAX == 4) {
+                        // field<double> at planet j from the shared factors:
+                        // term k = F(j, k) * (p_k - p_j) summed in k order; the
+                        // self term is gm / 1e-12 * (+0), a zero with gm's sign
+                        const double zs = __builtin_signbit(p.gm) ? -0.0 : 0.0;
+                        double ax = 0.0, ay = 0.0;
+#pragma unroll
+                        for (int k = 0; k < PMAX; ++k) {
+                            const bool self = k == j;
+                            const double tx = self ? zs : Fr[m][k] * (px[k] - pxj);
+                            const double ty = self ? zs : Fr[m][k] * (py[k] - pyj);
+                            if (k == 0) {
+                                ax = tx;
+                                ay = ty;
+                            } else {
+                                ax = k < np ? ax + tx : ax;
+                                ay = k < np ? ay + ty : ay;
+                            }
+                        }
+                        gx = ax;
+                        gy = ay;
+                    } else {
+                        field<double, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
+                    }
+#endif
+                    ndx = pdx + gx * p.dt;
+                    ndy = pdy + gy * p.dt;
+                }
+                v.x = T(wrap_unit<double>(pxj + p.dt * ndx));
+                v.y = T(wrap_unit<double>(pyj + p.dt * ndy));
+                v.z = T(ndx);
+                v.w = T(ndy);
+            }
+            out[m] = v;
+        }
+    }
+
+}
+
 // HELP: each step wave has a helper wave in its workgroup (waves QW..2QW-1)
 // that creates its finished games' next ones.  The step wave posts its
 // finished envs here as soon as it knows them -- before the surviving envs'
@@ -1748,6 +1883,29 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             uint32_t hkey = uint32_t(hh.w);
             const bool hk = kvalid || p.key_table != nullptr;
             if (q == 1 && !kvalid) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
+            // ... and, pair instance, the planet update of every env of the
+            // step wave (the survivors' stored after the post; the step wave
+            // then skips it: c3 12.39 -> 11.92 us with eight step waves per
+            // workgroup; the quad instance of config 2 keeps it, 5.45 vs 5.50)
+            constexpr bool PLANETS = LPE == 2;
+            const size_t NN = size_t(N);
+            V *planets = reinterpret_cast<V *>(st.planets);
+            constexpr int PPL = PMAX / LPE;
+            int np = hh.y & 0xff;
+            np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+            const bool t0 = (uint32_t(hh.x) & TICK_MASK) == 0;
+            const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
+            V hpv[PPL], hout[PPL];
+            T hpx[PPL], hpy[PPL];
+            if constexpr (PLANETS) {
+#pragma unroll
+                for (int m = 0; m < PPL; ++m) {   // (8 slots: a slot past np aliased to slot 0, as the step wave reads)
+                    const int j = q + LPE * m;
+                    hpv[m] = planets[size_t(PMAX > 4 ? (j < np ? j : 0) : (j < p.p_pad ? j : 0)) * NN + i];
+                    hpx[m] = hpv[m].x;
+                    hpy[m] = hpv[m].y;
+                }
+            }
             if (q < 2) {
                 uint32_t x = q == 0 ? hseed : hkey;
                 const uint32_t koff = q == 0 ? 0u : 397u;
@@ -1758,6 +1916,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 }
             }
             wave_sync();
+            if constexpr (PLANETS) planet_update<T, S, PMAX, LPE, PPL>(p, hpv, hpx, hpy, q, np, t0, slot_last, hout);
             // until the step wave posts (bounded: it always posts, the bound
             // only keeps a fault from hanging the device)
             for (uint32_t spin = 0; *reinterpret_cast<volatile uint32_t *>(&bx.flag) == 0 && spin < (1u << 22); ++spin)
@@ -1768,6 +1927,13 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #endif
             QuadCounts hc{};
             const uint64_t todo0 = bx.todo;
+            if (PLANETS && active && !((todo0 >> (lane & ~(LPE - 1))) & 1ull)) {   // a surviving env: its new planets
+#pragma unroll
+                for (int m = 0; m < PPL; ++m) {
+                    const int j = q + LPE * m;
+                    if (j < np) planets[size_t(j) * NN + i] = hout[m];
+                }
+            }
             if (todo0) {   // uniform
                 for (uint64_t todo = todo0; todo;)   // uniform
                     todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, s_chain,
@@ -2285,117 +2451,14 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             }
 
             STAMP(6);
-            // ---- own planets: gravity of all planets incl. self, in order
-            //      (core.py:289-294); float32 at tick 0 / for a lone planet
-            const float dtf = float(p.dt);
-            {   // the planets again from the quad (DPP) rather than 2*PMAX
-                // doubles held live across the bullet pass
-                T rx[PPL], ry[PPL];
+            // ---- own planets (core.py:289-294); the pair instance's helper waves do it
+            if constexpr (!(HELP && LPE == 2)) {
+                V pout[PPL];
+                planet_update<T, S, PMAX, LPE, PPL>(p, pv, mpx, mpy, q, np, t0, slot_last, pout);
 #pragma unroll
                 for (int m = 0; m < PPL; ++m) {
-                    rx[m] = mpx[m];
-                    ry[m] = mpy[m];
-                    asm volatile("" : "+v"(rx[m]), "+v"(ry[m]));
-                }
-                bcast_slots<T, PPL, LPE>(rx, px);
-                bcast_slots<T, PPL, LPE>(ry, py);
-            }
-            // Pair kernel, 4 slots: the float64 planet-planet factors
-            // gm / max(1e-12, d2) of the 6 distinct pairs, 3 per lane (d2 and
-            // so the factor are the same bit for bit both ways round), the
-            // partner's two by DPP; row i of lane q's planets i = q, q + 2 is
-            // then F(i, j) for j = 0..3 (see symmetric_rows)
-            double Fr[PPL][PMAX];
-            if constexpr (LPE == 2 && PMAX == 4) {
-                const bool l0 = q == 0;
-                // F(i, j) on lane 0, F(i1, j1) on lane 1: operands selected
-                // first, one division per lane
-                auto fac = [&](int i, int j, int i1, int j1) {
-                    const double ddx = (l0 ? px[j] : px[j1]) - (l0 ? px[i] : px[i1]);
-                    const double ddy = (l0 ? py[j] : py[j1]) - (l0 ? py[i] : py[i1]);
-                    return div_gravity(p.gm, max_floor(ddx * ddx + ddy * ddy));
-                };
-                // lane 0: A = F01, B = F03, C = F02; lane 1: A = F12, B = F23, C = F13
-                // (B is only read for planet slot 3: skipped when no env has it)
-                const double A = fac(0, 1, 1, 2);
-                const double B = slot_last ? fac(0, 3, 2, 3) : 0.0;
-                const double C = fac(0, 2, 1, 3);
-                const double A2 = pair_swap(A), B2 = pair_swap(B);   // lane 0: F12, F23; lane 1: F01, F03
-                const double z = 0.0;   // (self: unused)
-                // planet q:     lane 0 [-, F01, F02, F03]   lane 1 [F10, -, F12, F13]
-                // planet q + 2: lane 0 [F20, F21, -, F23]   lane 1 [F30, F31, F32, -]
-                Fr[0][0] = l0 ? z : A2;
-                Fr[0][1] = l0 ? A : z;
-                Fr[0][2] = l0 ? C : A;
-                Fr[0][3] = l0 ? B : C;
-                Fr[1][0] = l0 ? C : B2;
-                Fr[1][1] = l0 ? A2 : C;
-                Fr[1][2] = l0 ? z : B;
-                Fr[1][3] = l0 ? B2 : z;
-            }
-#pragma unroll
-            for (int m = 0; m < PPL; ++m) {
-                const int j = q + LPE * m;
-                if (j < np) {
-                    const double pxj = double(mpx[m]), pyj = double(mpy[m]);
-                    const double pdx = double(pv[m].z), pdy = double(pv[m].w);
-                    V v;
-                    if (np == 1) {
-                        // a lone planet's own field: r = +0, so gm / max(1e-12, 0) * r
-                        // is a zero with the sign of gm, exactly
-                        const float g0 = p.gm < 0.0 ? -0.0f : 0.0f;
-                        const float ndx = float(pdx) + g0 * dtf, ndy = float(pdy) + g0 * dtf;
-                        v.x = T(wrap_unit<float>(float(pxj) + dtf * ndx));
-                        v.y = T(wrap_unit<float>(float(pyj) + dtf * ndy));
-                        v.z = T(ndx);
-                        v.w = T(ndy);
-                    } else {
-                        double ndx, ndy;
-                        if (t0) {
-                            float gx, gy;
-                            field<float, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
-                            ndx = pdx + double(gx * dtf);
-                            ndy = pdy + double(gy * dtf);
-                        } else {
-                            double gx, gy;
-#ifdef ASTRO_ABLATE_PLANETFIELD   // timing ablation only (wrong results)
-                            gx = px[1] - pxj;
-                            gy = py[1] - pyj;
-#else
-                            if constexpr (LPE == 2 && PMAX == 4) {
-                                // field<double> at planet j from the shared factors:
-                                // term k = F(j, k) * (p_k - p_j) summed in k order; the
-                                // self term is gm / 1e-12 * (+0), a zero with gm's sign
-                                const double zs = __builtin_signbit(p.gm) ? -0.0 : 0.0;
-                                double ax = 0.0, ay = 0.0;
-#pragma unroll
-                                for (int k = 0; k < PMAX; ++k) {
-                                    const bool self = k == j;
-                                    const double tx = self ? zs : Fr[m][k] * (px[k] - pxj);
-                                    const double ty = self ? zs : Fr[m][k] * (py[k] - pyj);
-                                    if (k == 0) {
-                                        ax = tx;
-                                        ay = ty;
-                                    } else {
-                                        ax = k < np ? ax + tx : ax;
-                                        ay = k < np ? ay + ty : ay;
-                                    }
-                                }
-                                gx = ax;
-                                gy = ay;
-                            } else {
-                                field<double, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
-                            }
-#endif
-                            ndx = pdx + gx * p.dt;
-                            ndy = pdy + gy * p.dt;
-                        }
-                        v.x = T(wrap_unit<double>(pxj + p.dt * ndx));
-                        v.y = T(wrap_unit<double>(pyj + p.dt * ndy));
-                        v.z = T(ndx);
-                        v.w = T(ndy);
-                    }
-                    planets[size_t(j) * NN + is] = v;
+                    const int j = q + LPE * m;
+                    if (j < np) planets[size_t(j) * NN + is] = pout[m];
                 }
             }
 
@@ -2833,8 +2896,12 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
                                    dim3(int((int64_t(s.n_env) * 4 + 64 * QW_SMALL - 1) / (64 * QW_SMALL))),
                                    dim3(2 * 64 * QW_SMALL), 0, stream, p, s, drv, r, d, st, ar);
             else
-                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true>), dim3(grid),
-                                   dim3(2 * QBLOCK), 0, stream, p, s, drv, r, d, st, ar);
+            {   // (8 planet slots: four, a 16-wave workgroup would cap the 8-slot code at 128 VGPRs)
+                constexpr int W = PM > 4 ? 4 : QW_PAIR_HELP;
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true, W>),
+                                   dim3(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), dim3(2 * 64 * W), 0,
+                                   stream, p, s, drv, r, d, st, ar);
+            }
             return launched(lpe == 4 ? "astro_step(quad, helpers)" : "astro_step(pair, helpers)");
         }
         if (lpe == 4 && one)
