@@ -15,7 +15,12 @@
 //     private LDS set per wave, wave-scoped sync only).
 // Auto-reset runs inside the step (the finished envs' next games, created
 // wave-cooperatively); each env's generate_configs stream is an exact
-// MT19937 of any length (MTStream: cursor + the env's 624-word ring).
+// MT19937 of any length (MTStream: cursor + the env's 624-word ring).  A
+// one-tick launch of at most two step waves per SIMD gives each step wave a
+// helper wave in its workgroup (HelpBox): the helper makes the envs' next
+// games' MT19937 chains and -- pair instance -- their planet updates while
+// the step wave steps, then stores the survivors' planets and creates the
+// finished envs' next games once the step wave posts which envs finished.
 
 // What is computed is exactly astro/core.py's step (core.py:215-303) and
 // create (core.py:86-135), including the reference's numpy dtype behaviour:
