@@ -1409,10 +1409,11 @@ __device__ __forceinline__ bool quad_any(bool f, int lane) {
 #ifndef ASTRO_QUAD_WAVES
 #define ASTRO_QUAD_WAVES 4
 #endif
-// waves per workgroup of the small-N (quad) helper instance: config 2's 256
-// waves on 128 CUs, not 64 (c2 6.18 -> 5.52 us A/B; c3 wants four)
+// step waves per workgroup of the small-N (quad) helper instance: config
+// 2's 256 waves spread over more CUs (four: 6.18 us, two: 5.52, one: 5.31
+// with its helper, i.e. 128-thread workgroups; c3 wants eight, below)
 #ifndef ASTRO_QW_SMALL
-#define ASTRO_QW_SMALL 2
+#define ASTRO_QW_SMALL 1
 #endif
 constexpr int QW_SMALL = ASTRO_QW_SMALL;
 #ifndef ASTRO_QW_PAIR_HELP
@@ -1421,6 +1422,10 @@ constexpr int QW_SMALL = ASTRO_QW_SMALL;
 // step waves per workgroup of the pair instance with helpers (c3: eight,
 // 16-wave workgroups, 12.55 -> 12.13 us A/B; two: 13.12)
 constexpr int QW_PAIR_HELP = ASTRO_QW_PAIR_HELP;
+#ifndef ASTRO_QW_PAIR
+#define ASTRO_QW_PAIR 4
+#endif
+constexpr int QW_PAIR = ASTRO_QW_PAIR;   // 4-slot pair instance without helpers (1M: 4 = 111, 8 = 114, 16 = 131 us)
 #ifndef ASTRO_HELP_MAX_WAVES
 #define ASTRO_HELP_MAX_WAVES 2048
 #endif
@@ -1846,7 +1851,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
     __shared__ HelpBox s_box_all[HELP ? WPG : 1];
     __shared__ uint32_t s_pre_all[HELP ? WPG : 1][HELP ? QENV : 1][2][13 + 2 * S];   // a helper's chains, made ahead
-    static_assert(!HELP || (WPG > 1 && !OPAQUE), "helper waves: one-tick launches, several waves per workgroup");
+    // (wave_sync syncs one wave whenever the build's QW > 1, whatever this instance's WPG)
+    static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, wave-scoped LDS sync");
     const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
     const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
     float4 (*s_body)[NBOD2] = s_body_all[wv];
@@ -2915,9 +2921,12 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         else if (lpe == 4)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);
-        else if (one)
-            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2>), dim3(grid), dim3(QBLOCK), 0, stream, p,
+        else if (one) {
+            constexpr int W = PM > 4 ? QW : QW_PAIR;
+            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, false, W>),
+                               dim3(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), dim3(64 * W), 0, stream, p,
                                s, drv, r, d, st, ar);
+        }
         else
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 2>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);
