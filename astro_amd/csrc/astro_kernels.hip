@@ -1429,6 +1429,11 @@ constexpr int QW_PAIR = ASTRO_QW_PAIR;   // 4-slot pair instance without helpers
 #ifndef ASTRO_HELP_MAX_WAVES
 #define ASTRO_HELP_MAX_WAVES 2048
 #endif
+// s_setprio of a helper instance's step waves (0: left at the default, the
+// helpers' own priority)
+#ifndef ASTRO_STEP_PRIO
+#define ASTRO_STEP_PRIO 0
+#endif
 // Waves per quad-kernel workgroup.  The waves of a workgroup share nothing
 // (each has its own LDS rows and syncs only itself); four per workgroup make
 // a quarter as many workgroups for the dispatcher (launch floor 2.0 -> 1.6
@@ -1964,6 +1969,11 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #endif
             return hc;
         }
+#if ASTRO_STEP_PRIO > 0
+        // the step wave is the launch's critical path: let it win issue
+        // arbitration over its helper on the shared SIMD
+        __builtin_amdgcn_s_setprio(ASTRO_STEP_PRIO);
+#endif
     }
     const size_t BC = size_t(p.b_cap);
     V *ships = reinterpret_cast<V *>(st.ships);
