@@ -1917,7 +1917,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #pragma unroll
                 for (int m = 0; m < PPL; ++m) {   // (8 slots: a slot past np aliased to slot 0, as the step wave reads)
                     const int j = q + LPE * m;
-                    hpv[m] = planets[size_t(PMAX > 4 ? (j < np ? j : 0) : (j < p.p_pad ? j : 0)) * NN + i];
+                    hpv[m] = planets[size_t(j < np ? j : 0) * NN + i];
                     hpx[m] = hpv[m].x;
                     hpy[m] = hpv[m].y;
                 }
@@ -2005,11 +2005,19 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // round trip, which three waves per SIMD hide (c5: 56 B less per env,
     // time unchanged in the A/B)
     constexpr bool PLANETS_AFTER_HDR = PMAX > 4;
+    // With planets_only (config 3's 3-planet games) a filtered game never
+    // has a planet in the slots past it: those alias slot 0 (the line just
+    // read, no traffic; c3 reads 1 MB less per launch, 12.10 -> 12.03 us
+    // A/B) -- a kernarg bound, so the loads still go out with the header's.
+    // Pair instance with helpers only: the quad instance (c2) lost 2% to the
+    // fallback below, the helper-less pair instance (1M, rollouts) spilled
+    constexpr bool ALIAS = HELP && LPE == 2;
+    const int p_live = ALIAS && p.planets_only ? p.planets_only : p.p_pad;
     if constexpr (!PLANETS_AFTER_HDR) {
 #pragma unroll
         for (int m = 0; m < PPL; ++m) {
             const int j = q + LPE * m;
-            pv[m] = planets[size_t(j < p.p_pad ? j : 0) * NN + i];
+            pv[m] = planets[size_t(j < p_live ? j : 0) * NN + i];
         }
     }
     const int tick = int(uint32_t(h.x) & TICK_MASK);
@@ -2024,6 +2032,13 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         for (int m = 0; m < PPL; ++m) {
             const int j = q + LPE * m;
             pv[m] = planets[size_t(j < np ? j : 0) * NN + i];
+        }
+    }
+    else if (ALIAS && __builtin_amdgcn_readfirstlane(int(__any(np > p_live))) != 0) {   // uniform; only
+#pragma unroll                                                                         // a loaded state
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + LPE * m;
+            if (j >= p_live && j < np) pv[m] = planets[size_t(j) * NN + i];
         }
     }
 #pragma unroll
