@@ -9,12 +9,14 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
 NSTATS = 8
 KERNELS = {'auto': 0, 'lane': 1, 'quad': 2, 'pair': 3}
+ERRORS = {1: 'a helper wave never saw its step wave post (its finished games were not re-created)',
+          2: "a step wave never saw its helper's header read"}
 
 
 class AstroParams(ctypes.Structure):
@@ -59,6 +61,7 @@ class AstroState(ctypes.Structure):
         ('stream_ring', ctypes.c_void_p),
         ('n_env', ctypes.c_int32),
         ('state_f64', ctypes.c_int32),
+        ('errors', ctypes.c_void_p),
     ]
 
 

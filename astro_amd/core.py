@@ -9,12 +9,16 @@ the reference bit for bit (tests/test_gpu_parity.py): inputs are never
 mutated, a finished game returns ``(None, reward)`` with an int64 reward for
 a collision and a float32 reward for a timeout.
 
-This path is latency-bound by design (one tiny launch + copies per tick);
+This path is latency-bound by design: per tick one H2D copy of the packed
+state, one tiny launch, one D2H copy and a synchronisation (``_Shim``);
 bulk simulation belongs on :class:`astro_amd.env.BatchedEnv`.
 """
+import ctypes
+
 import numpy as np
 import torch
 
+from . import _lib
 from .config import (Bodies, Config, DEFAULT_CONFIG, Game, SOLO_CONFIG,  # noqa: F401
                      SOLO_EASY_CONFIG, State, Tick, generate_configs, nships)
 from .env import BatchedEnv
@@ -22,22 +26,59 @@ from .env import BatchedEnv
 _ENVS = {}
 
 
-def _device():
-    return torch.device('cuda', torch.cuda.current_device())
+class _Shim:
+    """One float64 game on the device for the single-game surface.  Its
+    state arrays live in ONE device buffer mirrored by one pinned host
+    buffer (BatchedEnv(arena=True)): a tick is one H2D copy of the input
+    (header, ships, planets, bullets, control, fire word), one launch, one
+    D2H copy of everything back, one synchronisation."""
+
+    def __init__(self, config, b_cap, device):
+        self.env = env = BatchedEnv(config, 1, device=device, b_cap=b_cap, dtype=torch.float64,
+                                    auto_reset=False, use_key_table=False, arena=True)
+        self.S = env.S
+        a = env.arena
+        self.h = {k: a.host_view(k) for k in a.layout}
+        self.in_bytes = a.end('fire')      # hdr .. fire: a tick's input
+        self.ctl_ptr = a.dev_view('control').data_ptr()
+        # the launch's schedule per (first tick of a game?, times out?):
+        # fire word = arena 'fire', timeout tick so `timeout` holds this call
+        self.params = {}
+        for tick in (0, 1):
+            for to in (False, True):
+                p = type(env.params).from_buffer_copy(env.params)
+                p.timeout_tick = tick if to else tick + 1
+                p.fire_bits = a.dev_view('fire').data_ptr()
+                self.params[tick, to] = p
+        self.stream = None
+
+    def state(self):
+        """Reference-shaped State from the host mirror (after a pull)."""
+        h = self.h
+        hdr = h['hdr'].view(np.uint32)
+        host = dict(ships=h['ships'].transpose(1, 0, 2), ships_b=h['ships_b'].transpose(1, 0),
+                    planets=h['planets'].transpose(1, 0, 2), bullets=h['bullets'],
+                    tick=hdr[:, 0] & 0x3fffff, nplanets=hdr[:, 1] & 0xff, nbullets=(hdr[:, 1] >> 16) & 0xffff,
+                    flags=(hdr[:, 1] >> 8) & 0xff)
+        return self.env.state_of(0, host)
+
+    def sync_pull(self):
+        self.env.arena.pull()
+        torch.cuda.current_stream(self.env.device).synchronize()
+        if self.h['errors'][0]:
+            self.env.check_errors()
 
 
-def _env(config, bullets_needed):
+def _shim(config, bullets_needed):
     key = (config._replace(seed=0), _device())
-    env = _ENVS.get(key)
-    if env is None or env.b_cap < bullets_needed:
-        cap = 64 if env is None else env.b_cap
+    sh = _ENVS.get(key)
+    if sh is None or sh.env.b_cap < bullets_needed:
+        cap = 64 if sh is None else sh.env.b_cap
         while cap < bullets_needed:
             cap *= 2
-        env = BatchedEnv(config, 1, device=key[1], b_cap=cap, dtype=torch.float64,
-                         auto_reset=False, use_key_table=False)
-        env._fire = torch.zeros(2, dtype=torch.int32, device=key[1])
-        _ENVS[key] = env
-    return env
+        sh = _Shim(config, cap, key[1])
+        _ENVS[key] = sh
+    return sh
 
 
 def create(config):
@@ -45,9 +86,10 @@ def create(config):
     seed = int(config.seed)
     if not 0 <= seed < 1 << 32:   # as np.random.RandomState(seed) (core.py:89) refuses it
         raise ValueError('Seed must be between 0 and 2**32 - 1')
-    env = _env(config, 0)
-    env.reset(seeds=[seed])
-    return env.state_of(0)
+    sh = _shim(config, 0)
+    sh.env.reset(seeds=[seed])
+    sh.sync_pull()
+    return sh.state()
 
 
 def step(state, control, config):
@@ -60,36 +102,45 @@ def step(state, control, config):
     if control.min() < -128 or control.max() > 127:
         raise ValueError('control codes must fit int8')
     nb = state.bullets.x.shape[0]
-    env = _env(config, nb + S)
+    sh = _shim(config, nb + S)
+    env, h = sh.env, sh.h
     # the reference's float64 bookkeeping for THIS call (core.py:257,263,267)
     timeout = config.max_time <= state.t + config.dt
     fire = config.reload_time <= state.reload + config.dt
     fresh = state.ships.x.dtype == np.float32      # create()'s float32 arrays
     tick = 0 if fresh else 1
     npl = state.planets.x.shape[0]
-    pl = np.concatenate([state.planets.x, state.planets.dx], 1).astype(np.float64)[None]
-    bl = np.concatenate([state.bullets.x, state.bullets.dx], 1).astype(np.float64)[None]
-    sh = np.concatenate([state.ships.x, state.ships.dx], 1).astype(np.float64)[None]
-    env.load_host(sh, np.asarray(state.ships.b, np.float64)[None], pl, bl,
-                  [tick], [npl], [nb])
-    env._fire.fill_(int(fire) << tick)
-    params = type(env.params).from_buffer_copy(env.params)
-    params.timeout_tick = tick if timeout else tick + 1
-    params.fire_bits = env._fire.data_ptr()
-    saved = env.params
-    env.params = params
-    try:
-        env.step(torch.as_tensor(control.astype(np.int8))[None], auto_reset=False)
-    finally:
-        env.params = saved
-    done = int(env.done[0].item())
-    reward = env.reward[0].cpu().numpy()
+    if npl > env.p_pad:
+        raise ValueError('a state holds more planets than max_planets')
+    # the input, written into the pinned mirror and sent in one copy
+    hdr = h['hdr'].view(np.uint32)
+    hdr[0, 0] = (int(hdr[0, 0]) & ~0x3fffff & 0xffffffff) | tick
+    hdr[0, 1] = npl | (nb << 16)
+    sx = h['ships']
+    sx[:, 0, 0:2] = state.ships.x
+    sx[:, 0, 2:4] = state.ships.dx
+    h['ships_b'][:, 0] = state.ships.b
+    h['planets'][:npl, 0, 0:2] = state.planets.x
+    h['planets'][:npl, 0, 2:4] = state.planets.dx
+    if nb:
+        h['bullets'][0, :nb, 0:2] = state.bullets.x
+        h['bullets'][0, :nb, 2:4] = state.bullets.dx
+    h['control'][0] = control
+    h['fire'][0] = int(fire) << tick
+    env.arena.push(sh.in_bytes)
+    rc = env.lib.astro_step(ctypes.byref(sh.params[tick, bool(timeout)]), ctypes.byref(env.state), sh.ctl_ptr,
+                            env.reward.data_ptr(), env.done.data_ptr(), None, 0,
+                            ctypes.c_void_p(torch.cuda.current_stream(env.device).cuda_stream))
+    if rc != 0:
+        _lib.check(rc, 'astro_step')
+    sh.sync_pull()
+    done = int(h['done'][0])
+    reward = h['reward'][0].copy()
     if done == 1:
         return None, reward.astype(np.int64)
     if done == 2:
         return None, reward.astype(np.float32)
-    h = env.to_host()
-    nxt = env.state_of(0, h)
+    nxt = sh.state()
     reload = state.reload + config.dt
     if fire:
         reload -= config.reload_time
@@ -97,8 +148,8 @@ def step(state, control, config):
     new = State(
         ships=Bodies(x=nxt.ships.x.astype(np.float64), dx=nxt.ships.dx.astype(np.float64),
                      b=nxt.ships.b.astype(np.float64)),
-        planets=Bodies(x=h['planets'][0, :npl, 0:2].astype(np.float32 if npl == 1 else np.float64),
-                       dx=h['planets'][0, :npl, 2:4].astype(np.float32 if npl == 1 else np.float64),
+        planets=Bodies(x=h['planets'][:npl, 0, 0:2].astype(np.float32 if npl == 1 else np.float64),
+                       dx=h['planets'][:npl, 0, 2:4].astype(np.float32 if npl == 1 else np.float64),
                        b=None),
         bullets=Bodies(x=nxt.bullets.x.astype(bdt), dx=nxt.bullets.dx.astype(bdt), b=None),
         reload=reload, t=state.t + config.dt)

@@ -1829,15 +1829,36 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
 // reset pass (~3.9k cycles) after its physics.
 struct HelpBox {
     uint32_t flag;                 // set (1) by the step wave once `todo` is written
-    uint32_t pad;
+    uint32_t seen;                 // set (nonzero) by the helper once its header load has returned
     unsigned long long todo;       // leader lanes (q == 0) of the finished envs
 };
 
 // Post a step wave's finished envs (leader lanes `todo`) to its helper.
 __device__ __forceinline__ void help_post(HelpBox &bx, uint64_t todo, int lane) {
+#ifdef ASTRO_DEBUG_DROP_POST   // fault-injection build only: the helper's wait must expire and report
+    (void)bx; (void)todo; (void)lane;
+    return;
+#endif
     if (lane == 0) bx.todo = todo;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the mask before the flag (LDS: in order per wave)
     if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.flag) = 1u;
+}
+
+// A bounded wait for an LDS word another wave of the workgroup sets: true
+// once it is nonzero, false when the bound (2^22 s_sleep 1, ~0.1 s) expires.
+// The bound only keeps a fault from hanging the device; an expired wait is
+// reported through the state's error word (report_error), never ignored.
+__device__ __forceinline__ bool wait_lds_word(const uint32_t &w) {
+    for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
+        if (*reinterpret_cast<const volatile uint32_t *>(&w) != 0u) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return *reinterpret_cast<const volatile uint32_t *>(&w) != 0u;
+}
+
+// Set bits of the state's device error word (AstroState.errors, optional).
+__device__ __forceinline__ void report_error(const AstroState &st, uint32_t bits, int lane) {
+    if (st.errors && lane == 0) atomicOr(st.errors, bits);
 }
 
 template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false, bool HELP = false,
@@ -1880,7 +1901,11 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         // one barrier; a wave past the last env returns after it, with its
         // helper)
         HelpBox &bx = s_box_all[wv];
-        if (helper && lane == 0) bx.flag = 0;
+        if (helper && lane == 0) {
+            bx.flag = 0;
+            bx.seen = 0;
+            bx.todo = 0;
+        }
         __syncthreads();
         if (base >= N) return QuadCounts{};
         if (helper) {
@@ -1894,6 +1919,11 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             constexpr int NW = 12 + 2 * S;
             uint32_t (*pre)[2][13 + 2 * S] = s_pre_all[wv];
             const int4 hh = reinterpret_cast<const int4 *>(st.hdr)[i];
+            // the step wave stores the survivors' new headers (tick + 1) at
+            // its end: it waits for this word, so the header read here is the
+            // launch's input whatever the memory system's timing (the store
+            // depends on the loaded value: it waits for the load's return)
+            if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.seen) = uint32_t(hh.x) | 1u;
             const uint32_t hseed = uint32_t(hh.z);
             const bool kvalid = (uint32_t(hh.x) & KEY_VALID) != 0;
             uint32_t hkey = uint32_t(hh.w);
@@ -1933,10 +1963,13 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             }
             wave_sync();
             if constexpr (PLANETS) planet_update<T, S, PMAX, LPE, PPL>(p, hpv, hpx, hpy, q, np, t0, slot_last, hout);
-            // until the step wave posts (bounded: it always posts, the bound
-            // only keeps a fault from hanging the device)
-            for (uint32_t spin = 0; *reinterpret_cast<volatile uint32_t *>(&bx.flag) == 0 && spin < (1u << 22); ++spin)
-                __builtin_amdgcn_s_sleep(1);
+            // until the step wave posts (bounded: it always posts; if the
+            // bound expires the mask is not trusted -- no stores, no resets --
+            // and the launch reports ASTRO_ERR_HELPER_WAIT)
+            if (!wait_lds_word(bx.flag)) {
+                report_error(st, ASTRO_ERR_HELPER_WAIT, lane);
+                return QuadCounts{};
+            }
             asm volatile("" ::: "memory");
 #ifdef ASTRO_STAMPS
             asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[20])::"memory");
@@ -2406,6 +2439,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         }
     }
     wave_sync();
+    if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
+        if (!wait_lds_word(s_box_all[wv].seen)) report_error(st, ASTRO_ERR_HEADER_WAIT, lane);
+    }
     const int wr_in = s_kept[e];
     const int hit_bits = s_hit[e];
     // the stores below recompute their addresses from an opaque copy of the
@@ -2835,6 +2871,7 @@ int check_state(const AstroState *s) {
     if (s->stream && !aligned16(s->stream)) return fail(-5, "stream must be 16-byte aligned");
     if (s->stream && (!s->stream_ring || (reinterpret_cast<uintptr_t>(s->stream_ring) & 3u)))
         return fail(-7, "the stream array needs its stream_ring ([n_env][624] uint32, 4-byte aligned)");
+    if (reinterpret_cast<uintptr_t>(s->errors) & 3u) return fail(-8, "errors must be 4-byte aligned");
     return 0;
 }
 
@@ -3033,10 +3070,14 @@ int dispatch(const AstroParams &p, const AstroState &s, A... a) {
 #define ASTRO_CASE(T, S, PM) \
     if (std::is_same<T, double>::value == bool(s.state_f64) && p.nships == S && pm == PM) \
         return L<T, S, PM>::run(p, s, a...);
+#ifdef ASTRO_ONLY_F32_S2   // A/B builds of the bench workloads only (tools/ab.py): a quarter of the compile time
+    ASTRO_CASE(float, 2, 4) ASTRO_CASE(float, 2, 8)
+#else
     ASTRO_CASE(float, 1, 4) ASTRO_CASE(float, 1, 8) ASTRO_CASE(float, 1, 16)
     ASTRO_CASE(float, 2, 4) ASTRO_CASE(float, 2, 8) ASTRO_CASE(float, 2, 16)
     ASTRO_CASE(double, 1, 4) ASTRO_CASE(double, 1, 8) ASTRO_CASE(double, 1, 16)
     ASTRO_CASE(double, 2, 4) ASTRO_CASE(double, 2, 8) ASTRO_CASE(double, 2, 16)
+#endif
 #undef ASTRO_CASE
     return fail(-20, "no kernel instance for this configuration");
 }

@@ -69,6 +69,47 @@ def key_table(device):
 QUAD_MAX_ENVS = 32768   # include/astro_step.h ASTRO_QUAD_MAX_ENVS
 
 
+class _Arena:
+    """Named arrays packed (16-byte aligned) into one device buffer, with a
+    pinned host mirror and numpy views of it: one H2D and one D2H copy move
+    them all."""
+
+    def __init__(self, specs, device):
+        self.layout = {}
+        off = 0
+        for name, shape, dt in specs:
+            nbytes = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            self.layout[name] = (off, shape, dt, nbytes)
+            off = (off + nbytes + 15) // 16 * 16
+        self.nbytes = off
+        self.dev = torch.zeros(off, dtype=torch.uint8, device=device)
+        self.host = torch.zeros(off, dtype=torch.uint8).pin_memory()
+        self.np = self.host.numpy()
+
+    def _view(self, buf, name):
+        off, shape, dt, nbytes = self.layout[name]
+        return buf[off:off + nbytes].view(dt).view(shape)
+
+    def dev_view(self, name):
+        return self._view(self.dev, name)
+
+    def host_view(self, name):
+        """numpy view of the pinned mirror (writes go out with push())."""
+        return self._view(self.host, name).numpy()
+
+    def end(self, name):
+        off, _, _, nbytes = self.layout[name]
+        return off + nbytes
+
+    def push(self, upto):
+        """Host mirror -> device, bytes [0, upto) (stream-ordered, async)."""
+        self.dev[:upto].copy_(self.host[:upto], non_blocking=True)
+
+    def pull(self):
+        """Device -> host mirror, every byte (stream-ordered, async)."""
+        self.host.copy_(self.dev, non_blocking=True)
+
+
 class BatchedEnv:
     """N lockstep games of one Config on one device.
 
@@ -91,7 +132,7 @@ class BatchedEnv:
 
     def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
                  dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto',
-                 use_key_table=True, planets_only=0):
+                 use_key_table=True, planets_only=0, arena=False):
         _schedule.check_config(config)
         planets_only = int(planets_only)
         if planets_only and (not 1 <= planets_only <= config.max_planets
@@ -118,16 +159,22 @@ class BatchedEnv:
 
         N, S, dev = self.n_env, self.S, self.device
         z = lambda *shape, dt=dtype: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
-        self.ships = z(S, N, 4)
-        self.ships_b = z(S, N)
-        self.planets = z(self.p_pad, N, 4)
-        self.bullets = z(N, self.b_cap, 4)
-        self.hdr = z(N, 4, dt=torch.int32)
+        # the arrays a tick reads and writes; with arena=True they are views of
+        # ONE device buffer mirrored by one pinned host buffer, so a host that
+        # owns the state (the single-game shim, astro_amd.core) moves a tick's
+        # input and output with one copy each way
+        specs = (('hdr', (N, 4), torch.int32), ('ships', (S, N, 4), dtype), ('ships_b', (S, N), dtype),
+                 ('planets', (self.p_pad, N, 4), dtype), ('bullets', (N, self.b_cap, 4), dtype),
+                 ('control', (N, S), torch.int8), ('fire', (2,), torch.int32),
+                 ('reward', (N, S), torch.float32), ('done', (N,), torch.uint8), ('errors', (1,), torch.int32))
+        self.arena = _Arena(specs, dev) if arena else None
+        for name, shape, dt in specs:
+            if name not in ('control', 'fire'):
+                setattr(self, name, self.arena.dev_view(name) if arena else z(*shape, dt=dt))
         self.stream = z(N, 4, dt=torch.int32)
         self.stream_ring = z(N, MT_N, dt=torch.int32)
-        self.reward = z(N, S, dt=torch.float32)
-        self.done = z(N, dt=torch.uint8)
         self.stats = z(max(1, (N + 15) // 16), _lib.NSTATS, dt=torch.int64)
+        # (errors: AstroState.errors, the ASTRO_ERR_* bits a faulting launch sets)
         self.fire_bits = torch.from_numpy(self.schedule.fire_bits().view(np.int32)).to(dev)
 
         k = _schedule.kernel_constants(config)
@@ -141,7 +188,7 @@ class BatchedEnv:
             planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),
             hdr=self.hdr.data_ptr(), stream=self.stream.data_ptr(),
             stream_ring=self.stream_ring.data_ptr(),
-            n_env=N, state_f64=1 if dtype == torch.float64 else 0)
+            n_env=N, state_f64=1 if dtype == torch.float64 else 0, errors=self.errors.data_ptr())
 
         self.stream_seeds = _shard.stream_seeds(config, self.env_offset, N)
         seeds_t = torch.from_numpy(self.stream_seeds.view(np.int32)).to(dev)
@@ -182,6 +229,7 @@ class BatchedEnv:
             raise ValueError('control must be [%d, %d], got %s' % (self.n_env, self.S, tuple(c.shape)))
         self.launch(c.data_ptr(), auto_reset, stats)
         self._ctl = c
+        self._last = (self.reward, self.done)
         return self.obs(), self.reward, self.done
 
     def launch(self, control_ptr, auto_reset=None, stats=True, stream=None):
@@ -227,13 +275,42 @@ class BatchedEnv:
     def nbullets(self):
         return (self.hdr[:, 1] >> 16) & 0xffff
 
+    def launch_waves(self):
+        """(step waves, helper waves) of one astro_step launch of this batch:
+        the library's rule (launch_step in astro_kernels.hip) -- a one-tick
+        auto-reset launch of at most 2,048 quad/pair step waves gets one
+        helper wave per step wave (HelpBox)."""
+        lpe = dict(lane=1, quad=4, pair=2)[self.step_kernel]
+        sw = (self.n_env * lpe + 63) // 64
+        help_ = lpe > 1 and self.auto_reset and self.n_env * lpe <= 64 * 2048
+        return sw, sw if help_ else 0
+
+    def device_errors(self, clear=True):
+        """The ASTRO_ERR_* bits any launch since the last check set (0: none;
+        synchronises).  Every bit means a launch detected an internal fault
+        and the state it wrote is not trusted."""
+        v = int(self.errors.item())
+        if v and clear:
+            self.errors.zero_()
+        return v
+
+    def check_errors(self):
+        """Raise AstroError if a launch since the last check reported a fault."""
+        v = self.device_errors()
+        if v:
+            why = '; '.join(m for b, m in sorted(_lib.ERRORS.items()) if v & b) or 'unknown'
+            raise _lib.AstroError('astro_step reported device error 0x%x: %s' % (v, why))
+
     def info(self):
-        """Per-env flags of the last step (SURVEY section 8b's info): ``hit``
-        uint8 bitmask of the ships a collision hit (bit s: reward[s] == -1 on
-        a collision, core.py:253-255), ``overflow`` the env's current game
-        has dropped a bullet for lack of b_cap, ``create_exhausted`` its
-        create() needed more than 227 MT19937 words (never in practice)."""
-        hit = ((self.reward < 0) & (self.done == 1)[:, None]).to(torch.uint8)
+        """Per-env flags of the last step or rollout tick (SURVEY section 8b's
+        info): ``hit`` uint8 bitmask of the ships a collision hit (bit s:
+        reward[s] == -1 on a collision, core.py:253-255), ``overflow`` the
+        env's current game has dropped a bullet for lack of b_cap,
+        ``create_exhausted`` its create() needed more than 227 MT19937 words
+        (never in practice).  Raises if a launch reported a device fault."""
+        self.check_errors()
+        reward, done = getattr(self, '_last', (self.reward, self.done))
+        hit = ((reward < 0) & (done == 1)[:, None]).to(torch.uint8)
         hit = (hit << torch.arange(self.S, device=self.device, dtype=torch.uint8)[None, :]).sum(1)
         fl = self.flags
         return dict(hit=hit.to(torch.uint8), overflow=(fl & 1) != 0, create_exhausted=(fl & 2) != 0)
@@ -310,6 +387,7 @@ class BatchedEnv:
             None if ctl is None else ctl.data_ptr(), reward.data_ptr(), done.data_ptr(),
             self.stats.data_ptr() if stats else None, int(ar), _stream_ptr(self.device)), 'astro_rollout')
         self._keep_rollout = ctl
+        self._last = (reward[-1], done[-1])   # info() describes the last tick
         return reward, done
 
     def play(self, bots, games=1, chunk=256, max_ticks=None, script_args=None):
@@ -380,12 +458,15 @@ class BatchedEnv:
 
     def stat_dict(self):
         v = self.stats.sum(0).cpu().tolist()
+        self.check_errors()
         return dict(zip(_lib.STAT_NAMES, v))
 
     # ----------------------------------------------------- host import/export
 
     def to_host(self):
-        """Every array as numpy (synchronises)."""
+        """Every array as numpy (synchronises; raises if a launch reported a
+        device fault)."""
+        self.check_errors()
         return dict(ships=self.ships.permute(1, 0, 2).cpu().numpy(),
                     ships_b=self.ships_b.permute(1, 0).cpu().numpy(),
                     planets=self.planets.permute(1, 0, 2).cpu().numpy(),
@@ -393,8 +474,11 @@ class BatchedEnv:
                     tick=self.tick.cpu().numpy(), nplanets=self.nplanets.cpu().numpy(),
                     nbullets=self.nbullets.cpu().numpy(), flags=self.flags.cpu().numpy())
 
-    def load_host(self, ships, ships_b, planets, bullets, tick, nplanets, nbullets):
-        """Overwrite the state from host arrays (env-major, like to_host)."""
+    def load_host(self, ships, ships_b, planets, bullets, tick, nplanets, nbullets, flags=None):
+        """Overwrite the state from host arrays (env-major, like to_host).
+        ``flags`` (to_host's) are the loaded games' flag bits; default 0 (a
+        loaded game has dropped no bullet).  Each env's seed stream and its
+        pending next game are kept."""
         dev, dt = self.device, self.dtype
 
         def put(dst, src):
@@ -415,7 +499,8 @@ class BatchedEnv:
         old = self.hdr.cpu().numpy().view(np.uint32).astype(np.int64)
         hdr = old.copy()
         hdr[:, 0] = (old[:, 0] & ~TICK_MASK & 0xFFFFFFFF) | np.asarray(tick, np.int64)
-        hdr[:, 1] = np.asarray(nplanets, np.int64) | (old[:, 1] & 0xff00) | (nb << 16)
+        fl = np.zeros(self.n_env, np.int64) if flags is None else np.asarray(flags, np.int64) & 0xff
+        hdr[:, 1] = np.asarray(nplanets, np.int64) | (fl << 8) | (nb << 16)
         self.hdr.copy_(torch.as_tensor(hdr.astype(np.uint32).view(np.int32)).to(dev))
 
     def state_of(self, i, host=None):

@@ -3,7 +3,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3]
 
-One process per GPU (torchrun for N > 1).  Each rank steps its own shard of
+One process per GPU: under torchrun (WORLD_SIZE set) this process is one
+rank; with --gpus N > 1 and no launcher it starts the N ranks itself (one
+child per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, RCCL) and never
+touches the GPU.  Each rank steps its own shard of
 envs (global env ids, no collective on the hot path); a "step" is one
 astro_step launch = one tick of every env on that GPU, auto-reset included.
 Controls are synthetic uniform random actions in [0, 6), keyed by (global
@@ -14,6 +17,8 @@ import argparse
 import json
 import multiprocessing as mp
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -114,6 +119,111 @@ def algorithmic_bytes(env, dstats, launches):
     return (fixed + var) / launches
 
 
+def single_game_latency(cfg, ticks=2000, seed=0):
+    """The single-game drop-in (astro_amd.core, what astro/server.py's
+    game_tick and core.play's loop call): us per core.step tick with random
+    controls, re-creating on termination, and us per tick of core.play with
+    two random bots (Bots.control + step + Tick bookkeeping)."""
+    from astro_amd import core
+    rng = np.random.RandomState(seed)
+    state = core.create(cfg)
+    for _ in range(50):   # first calls: the shim's buffers, the kernels' first launch
+        state, _ = core.step(state, rng.randint(0, 6, size=2), cfg)
+        if state is None:
+            state = core.create(cfg)
+    n_create = 0
+    t0 = time.perf_counter()
+    for _ in range(ticks):
+        state, _ = core.step(state, rng.randint(0, 6, size=2), cfg)
+        if state is None:
+            state = core.create(cfg)
+            n_create += 1
+    dt = time.perf_counter() - t0
+    bot = lambda s: int(rng.randint(0, 6))  # noqa: E731
+    played = 0
+    t1 = time.perf_counter()
+    k = 0
+    while played < ticks:
+        g = core.play(cfg._replace(seed=k), [bot, bot])
+        played += len(g.ticks)
+        k += 1
+    dp = time.perf_counter() - t1
+    return dict(us_per_step=dt / ticks * 1e6, steps=ticks, creates=n_create, us_per_play_tick=dp / played * 1e6,
+                play_ticks=played, games=k,
+                path='astro_amd.core.step: one H2D copy of the packed state, one launch, one D2H copy, '
+                     'one synchronisation per tick (float64 state, bit-exact to the reference)')
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """--gpus N without a launcher: start N ranks of this script, one per
+    GPU, as ``torch.distributed.run --nproc-per-node N`` would (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT); rank 0
+    prints the line.  This process never initialises HIP (a parent that had
+    would pass its GPU state to no one and hold a device context).  A rank
+    that fails ends the others; the exit code is the first failure's."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:       # the rest would wait in a collective for ever
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def stub_rank(args, world, rank):
+    """--stub: the rank body without a GPU (tests of the launcher on CPU):
+    the same process group, barrier and max/sum-over-ranks reductions as a
+    real rank, then rank 0's one JSON line."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(os.environ.get('ASTRO_DIST_BACKEND', 'gloo'))
+        dist.barrier()
+    wall = _shard.max_over_ranks(0.001 * (1 + rank))
+    n_ranks = int(_shard.sum_over_ranks([1])[0])
+    if rank == 0:
+        print(json.dumps(dict(metric=METRIC, value=0.0, unit='env-steps/s', n_gpus=0, ranks=n_ranks,
+                              steps=args.steps, warmup=args.warmup, ms_per_step=wall / max(1, args.steps) * 1e3,
+                              higher_is_better=True, scaling='weak', vs_baseline=None, stub=True)), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+PROFILE_ROUNDS = ('round3', 'round2')
+
+
+def profile_file(name):
+    """The newest committed profile of that name (profiles/round3, then round2)."""
+    for r in PROFILE_ROUNDS:
+        p = os.path.join(ROOT, 'profiles', r, name)
+        if os.path.exists(p):
+            return p
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -141,13 +251,22 @@ def main():
                     help='secondary line: the workload as K-tick rollouts with the on-device random '
                          'policy, K ticks per launch (0 = skip)')
     ap.add_argument('--no-features', action='store_true', help='skip the observation-builder line')
+    ap.add_argument('--eager-head', type=int, default=2,
+                    help='timed launches issued eagerly before the graph replays (the GPU runs them while '
+                         'the host submits the first graph, so it never idles at the start of the region)')
+    ap.add_argument('--no-single', action='store_true', help='skip the single-game drop-in latency line')
+    ap.add_argument('--stub', action='store_true', help=argparse.SUPPRESS)   # launcher test: no GPU work
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    if args.stub:
+        return stub_rank(args, world, rank)
     # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal)
     # ranks share devices and ASTRO_DIST_BACKEND=gloo avoids RCCL's one-rank-per-GPU rule
     dev = torch.device('cuda', local % max(1, torch.cuda.device_count()))
@@ -182,43 +301,54 @@ def main():
             import torch.distributed as dist
             dist.barrier()
 
+    # settle: a few eager launches of the one-tick instance after the burn-in's
+    # rollout instance (the first launch after the switch is the slow one),
+    # then the W warmup launches
+    settle = 3
+    for t in range(settle):
+        env.launch(ptrs[t % max(1, ticks)])
     for t in range(args.warmup):
         env.launch(ptrs[t])
     barrier()
 
-    # Timed region: every one of the K launches has its own control buffer;
-    # with --graph G they are captured G at a time into hipGraphs (capture
-    # launches nothing) so the host's per-launch cost is out of the loop.
+    # Timed region: every one of the K launches has its own control buffer.
+    # The first `eager_head` are launched eagerly, the rest were captured G at
+    # a time into hipGraphs (capture launches nothing), so the host's
+    # per-launch cost is out of the loop and the GPU runs the eager head while
+    # the host submits the first graph.  Each graph is replayed once, untimed,
+    # before the region: its first replay uploads it.
+    head = min(args.steps, max(0, args.eager_head)) if args.graph > 0 else args.steps
     graphs = []
-    if args.graph > 0:
+    if args.graph > 0 and head < args.steps:
         cap = torch.cuda.Stream(dev)
         cap.wait_stream(stream)
         with torch.cuda.stream(cap):
-            for g0 in range(0, args.steps, args.graph):
+            for g0 in range(head, args.steps, args.graph):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cap):
                     for k in range(g0, min(args.steps, g0 + args.graph)):
                         env.launch(ptrs[args.warmup + k])
                 graphs.append(g)
         stream.wait_stream(cap)
+        for g in graphs:
+            g.replay()
     barrier()
     s0 = env.stat_dict()
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    if graphs:
-        for g in graphs:
-            g.replay()
-    else:
-        for k in range(args.steps):
-            env.launch(ptrs[args.warmup + k])
+    for k in range(head):
+        env.launch(ptrs[args.warmup + k])
+    for g in graphs:
+        g.replay()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     barrier()
     s1 = env.stat_dict()
     gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
+    dev_err = env.device_errors()
 
     # Kernel duration: launches timed one by one (hipEvent pair around each,
     # on the launch stream), continuing the same games with fresh controls.
@@ -279,7 +409,8 @@ def main():
     fl = env.flags
     tot = _shard.sum_over_ranks([d[k] for k in ('bullets_in', 'resets', 'overflows', 'collisions',
                                                 'timeouts')]
-                                + [int(((fl & 1) != 0).sum()), int(((fl & 2) != 0).sum())], device=red_dev)
+                                + [int(((fl & 1) != 0).sum()), int(((fl & 2) != 0).sum()), dev_err],
+                                device=red_dev)
     # distinct devices behind the ranks (a one-GPU rehearsal shares one)
     n_dev = int(_shard.sum_over_ranks([1 if local < torch.cuda.device_count() else 0], device=red_dev)[0])
     bytes_launch = algorithmic_bytes(env, d, args.steps)
@@ -299,33 +430,50 @@ def main():
         mlb = tot[0] / (n_total * args.steps)
         rps = tot[1] / args.steps
 
-        def matching(path):
-            if not os.path.exists(path):
+        def matching(path, override=''):
+            path = override or path
+            if not path or not os.path.exists(path):
                 return None
             with open(path) as f:
                 j = json.load(f)
+            j['_path'] = os.path.relpath(path, ROOT)
             ok = (j.get('n_env') == n and j.get('kernel') in (args.kernel, 'auto', env.step_kernel)
                   and abs(j.get('mean_live_bullets', -1) - mlb) <= 0.1 * max(mlb, 0.05) + 1e-9
                   and abs(j.get('resets_per_step', -1) - rps) <= 0.1 * max(rps, 1.0))
             return j if ok else None
         traffic = None
-        tj = matching(args.traffic or os.path.join(ROOT, 'profiles', 'round2', 'traffic_%s_%s.json' % (
-            args.workload, args.state)))
+        tj = matching(profile_file('traffic_%s_%s.json' % (args.workload, args.state)), args.traffic)
         if tj:
             traffic = tj.get('hbm_bytes_per_launch')
         # secondary bound: VALU issue, from the committed PMC instruction count
-        # of this workload's kernel (profiles/round2/pmc_<workload>_<state>.json)
+        # of this workload's kernel (profiles/round*/pmc_<workload>_<state>.json).
+        # SQ_WAVES / SQ_INSTS_VALU count every wave of the launch: with helper
+        # waves (HelpBox) that is step and helper waves together, so the
+        # per-launch total is what is compared with the issue peak, and the
+        # per-wave figure is an average over both roles
         issue = None
-        pj = matching(os.path.join(ROOT, 'profiles', 'round2', 'pmc_%s_%s.json' % (args.workload, args.state)))
+        pj = matching(profile_file('pmc_%s_%s.json' % (args.workload, args.state)))
         if pj:
             lpe = dict(lane=1, quad=4, pair=2)[env.step_kernel]
             if pj.get('lanes_per_env') == lpe:
-                rate = pj['waves'] * pj['valu_per_wave'] / (launch_ms * 1e-3)
+                valu_launch = pj['waves'] * pj['valu_per_wave']
+                rate = valu_launch / (launch_ms * 1e-3)
                 peak = 256 * 4 * 2.4e9 / 4
+                sw, hw = env.launch_waves()
+                per_simd = sw / 1024.0
+                frac_i = rate / peak
+                note = ('%d step waves (%.2f per SIMD)%s; %s' % (
+                    sw, per_simd, (' + %d helper waves' % hw) if hw else '',
+                    'issue-bound' if frac_i > 0.8 else
+                    ('partly issue-bound: VALU issue %.0f%% of peak, the rest latency (DESIGN.md section 3)' % (
+                        100 * frac_i) if frac_i > 0.45 else
+                     'latency-bound: VALU issue %.0f%% of peak at %.1f waves per SIMD (DESIGN.md section 3)' % (
+                         100 * frac_i, (sw + hw) / 1024.0))))
                 issue = dict(bound='valu-issue', achieved=rate, peak=peak, unit='wave-instructions/s',
-                             frac=rate / peak, valu_per_wave=pj['valu_per_wave'], waves=pj['waves'],
-                             note='not HBM-bound and not issue-bound: two waves per SIMD at c3, '
-                                  'latency-bound (DESIGN.md section 3)')
+                             frac=frac_i, valu_per_launch=valu_launch,
+                             f64_per_launch=pj['waves'] * pj.get('f64_per_wave', 0.0),
+                             waves_counted=pj['waves'], step_waves=sw, helper_waves=hw,
+                             valu_per_wave_both_roles=pj['valu_per_wave'], source=pj.get('_path'), note=note)
         out = dict(
             metric=METRIC, value=value, unit='env-steps/s', n_gpus=n_dev, ranks=world, steps=args.steps,
             warmup=args.warmup, ms_per_step=wall_max / args.steps * 1e3, higher_is_better=True,
@@ -344,10 +492,11 @@ def main():
                           timing='hipEvent pair around the timed region / K launches'),
             issue_roofline=issue,
             gpu_ms_per_step=gpu_ms_per_step,
-            timed_region='%d launches, %s' % (
-                args.steps, ('replayed as %d hipGraph(s) of up to %d launches' % (len(graphs), args.graph))
-                if graphs else 'launched eagerly'),
-            burn_in_ticks=args.burn_in,
+            timed_region='%d launches: %d eager, then %s' % (
+                args.steps, head, ('%d hipGraph replay(s) of up to %d launches, each graph replayed once '
+                                   'untimed before the region' % (len(graphs), args.graph)) if graphs else 'no graph'),
+            burn_in_ticks=args.burn_in, settle_launches=settle,
+            device_errors=int(tot[7]),
             stats=dict(mean_live_bullets=mlb,
                        serial_resets_per_step=d.get('serial_resets', 0) / args.steps,
                        resets_per_step=rps, overflow_bullets=tot[2],
@@ -356,15 +505,22 @@ def main():
                        envs_flag_overflow=tot[5], envs_flag_create_exhausted=tot[6]),
         )
         out.update(extras)
+        if world == 1 and not args.no_single:
+            out['single_game'] = single_game_latency(DEFAULT_CONFIG)
         if world == 1 and not args.no_cpu:
             procs = args.cpu_procs or cpu_share()
             out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, procs, wl['planets_only'])
             out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']
+            if 'single_game' in out:   # the port's own per-tick time, one core
+                out['single_game']['cpu_port_us_per_step'] = 1e6 / out['cpu_baseline']['per_core']
         print(json.dumps(out), flush=True)
+        if int(tot[7]):
+            raise SystemExit('bench: a launch reported device error bits (device_errors=%d): the state '
+                             'and the line above are not trusted' % int(tot[7]))
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main() or 0)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 12
+#define ASTRO_ABI_VERSION 13
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -112,7 +112,18 @@ typedef struct AstroState {
                               writes it before it reads it, no initialisation needed */
     int32_t n_env;
     int32_t state_f64;  /* 0: float arrays, 1: double arrays */
+    uint32_t *errors;   /* optional (NULL = not reported): a device word the kernels OR
+                           ASTRO_ERR_* bits into when a launch detects an internal fault;
+                           the caller clears it and reads it after the launches (the
+                           state written by a launch that set a bit is not trusted) */
 } AstroState;
+
+/* Bits of AstroState.errors. */
+enum {
+    ASTRO_ERR_HELPER_WAIT = 1,  /* a helper wave's wait for its step wave's post expired:
+                                   that wave's finished games were not re-created */
+    ASTRO_ERR_HEADER_WAIT = 2   /* a step wave's wait for its helper's header read expired */
+};
 
 /* Control sources of astro_rollout / astro_controls. */
 enum {

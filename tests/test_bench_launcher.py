@@ -1,0 +1,51 @@
+"""bench.py's own rank launcher, on CPU (gloo, a stub rank body).
+
+``python bench.py --gpus N`` without torchrun starts N ranks itself (one
+child per GPU with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), so the driver's
+multi-GPU run measures configs 4 and 5 however it is invoked.  ``--stub``
+swaps the GPU body for the same process group, barrier and reductions."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None):
+    env = dict(os.environ, ASTRO_DIST_BACKEND='gloo', PYTHONDONTWRITEBYTECODE='1')
+    env.pop('WORLD_SIZE', None)
+    env.pop('RANK', None)
+    env.pop('LOCAL_RANK', None)
+    env.update(extra_env or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith('{')]
+    return p, lines
+
+
+def test_self_launched_ranks_print_one_line():
+    p, lines = _run(['--gpus', '2', '--steps', '7', '--stub'])
+    assert p.returncode == 0, p.stderr
+    assert len(lines) == 1, p.stdout
+    j = json.loads(lines[0])
+    assert j['ranks'] == 2 and j['steps'] == 7 and j['stub']
+    # max over ranks of the stub's per-rank wall (1 ms * (1 + rank))
+    assert abs(j['ms_per_step'] - 2.0 / 7) < 1e-9
+
+
+def test_four_ranks_and_single_rank():
+    p, lines = _run(['--gpus', '4', '--stub'])
+    assert p.returncode == 0, p.stderr
+    assert len(lines) == 1 and json.loads(lines[0])['ranks'] == 4
+    p, lines = _run(['--gpus', '1', '--stub'])
+    assert p.returncode == 0, p.stderr
+    assert len(lines) == 1 and json.loads(lines[0])['ranks'] == 1
+
+
+def test_failing_rank_ends_the_launch():
+    """A rank that cannot join (bad backend name) fails the whole launch
+    with a nonzero code instead of leaving the others waiting."""
+    p, lines = _run(['--gpus', '2', '--stub'], {'ASTRO_DIST_BACKEND': 'no-such-backend'})
+    assert p.returncode != 0
+    assert lines == []

@@ -411,6 +411,51 @@ def test_config4_eight_shards_compose():
     assert int(full.stat_dict()['resets']) > 0
 
 
+def test_config5_full_size_instances_agree():
+    """BASELINE config 5 per GPU exactly as bench.py's c5 runs it: 131,072
+    envs, max_planets 8 (1-8 planets, p_pad 8), bullets on, auto-reset, 200
+    ticks.  The instance the bench times -- AUTO = pair kernel WITHOUT helper
+    waves (4,096 step waves, more than two per SIMD) -- equals two 65,536-env
+    shards (pair kernel WITH helper waves) and the lane kernel, bit for bit,
+    on every array (headers, stream cursors and rings, ships, planets,
+    bullets).  (create() draws the planet count from the seed's first word,
+    core.py:90: the batch holds every count 1..8.)"""
+    from astro_amd import BatchedEnv
+    cfg = CFG['default']._replace(max_planets=8)
+    n, ticks = 131072, 200
+    g = torch.Generator(device='cuda').manual_seed(5)
+    ctls = torch.randint(0, 6, (ticks, n, 2), generator=g, device='cuda', dtype=torch.int8)
+
+    def run(offset, count, kernel='auto'):
+        env = BatchedEnv(cfg, count, device='cuda:0', b_cap=32, p_pad=8, env_offset=offset, kernel=kernel)
+        env.reset()
+        for t in range(ticks):
+            env.launch(ctls[t, offset:offset + count].contiguous().data_ptr())
+        torch.cuda.synchronize()
+        env.check_errors()
+        return env
+    full = run(0, n)
+    assert full.step_kernel == 'pair' and full.launch_waves() == (4096, 0)
+    np_ = full.nplanets
+    assert int(np_.min()) == 1 and int(np_.max()) == 8
+    st = full.stat_dict()
+    assert st['resets'] > 10000 and st['bullets_in'] > 0
+    arrays = ('hdr', 'stream', 'stream_ring', 'bullets')      # [N, ...]
+    slot_major = ('ships', 'ships_b', 'planets')              # [slot, N, ...]
+    for r in range(2):
+        half = run(r * (n // 2), n // 2)
+        assert half.launch_waves() == (2048, 2048)
+        sl = slice(r * (n // 2), (r + 1) * (n // 2))
+        for f in arrays:
+            assert torch.equal(getattr(half, f), getattr(full, f)[sl]), (r, f)
+        for f in slot_major:
+            assert torch.equal(getattr(half, f), getattr(full, f)[:, sl]), (r, f)
+        del half
+    lane = run(0, n, kernel='lane')
+    for f in arrays + slot_major:
+        assert torch.equal(getattr(lane, f), getattr(full, f)), f
+
+
 @pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('tick', [0, 7])
 def test_near_threshold_collisions_exact(tick, kernel):
