@@ -26,6 +26,10 @@ from .env import BatchedEnv
 _ENVS = {}
 
 
+def _device():
+    return torch.device('cuda', torch.cuda.current_device())
+
+
 class _Shim:
     """One float64 game on the device for the single-game surface.  Its
     state arrays live in ONE device buffer mirrored by one pinned host

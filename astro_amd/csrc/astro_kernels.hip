@@ -1753,6 +1753,55 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
         Fr[1][2] = l0 ? z : B;
         Fr[1][3] = l0 ? B2 : z;
     }
+    // Pair kernel, 8 slots (config 5): the 28 distinct pair factors, 14 per
+    // lane instead of 32 (each own planet's 8 terms), exchanged by DPP.
+    // Lane q owns planets q + 2m (m < 4): the 6 pairs among its own planets
+    // it computes alone (Sf); the 16 pairs of an own planet with a partner
+    // planet (Xf[m][j] = F(own m, partner planet j), planet j of the other
+    // lane = 2j + 1 - q) are split: pair (a, b), a != b, computed by both
+    // lanes at once -- lane 0 F(2a, 2b + 1), lane 1 F(2a + 1, 2b) -- gives
+    // each lane Xf[a][b] and, from the other lane, Xf[b][a]; the 4 diagonal
+    // pairs (2a, 2a + 1) two per lane, swapped likewise.
+    if constexpr (LPE == 2 && PMAX == 8) {
+        const bool l0 = q == 0;
+        auto fac = [&](double ax, double ay, double bx, double by) {
+            const double dx = bx - ax, dy = by - ay;   // (either sign: d2 is the same bit for bit)
+            return div_gravity(p.gm, max_floor(dx * dx + dy * dy));
+        };
+        double ox[PPL], oy[PPL], tx[PPL], ty[PPL];   // own planets; the other lane's
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            ox[m] = double(mpx[m]);
+            oy[m] = double(mpy[m]);
+            tx[m] = l0 ? px[2 * m + 1] : px[2 * m];
+            ty[m] = l0 ? py[2 * m + 1] : py[2 * m];
+        }
+        double Sf[PPL][PPL], Xf[PPL][PPL];
+#pragma unroll
+        for (int a = 0; a < PPL; ++a) {
+            Sf[a][a] = 0.0;   // (self: unused)
+#pragma unroll
+            for (int b = a + 1; b < PPL; ++b) {
+                Sf[a][b] = Sf[b][a] = fac(ox[a], oy[a], ox[b], oy[b]);
+                const double v = fac(ox[a], oy[a], tx[b], ty[b]);
+                Xf[a][b] = v;
+                Xf[b][a] = pair_swap(v);
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < PPL / 2; ++d) {   // lane 0: pair (4d, 4d + 1), lane 1: (4d + 2, 4d + 3)
+            const double v = fac(l0 ? ox[2 * d] : ox[2 * d + 1], l0 ? oy[2 * d] : oy[2 * d + 1],
+                                 l0 ? tx[2 * d] : tx[2 * d + 1], l0 ? ty[2 * d] : ty[2 * d + 1]);
+            const double w = pair_swap(v);
+            Xf[2 * d][2 * d] = l0 ? v : w;
+            Xf[2 * d + 1][2 * d + 1] = l0 ? w : v;
+        }
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+#pragma unroll
+            for (int k = 0; k < PMAX; ++k) Fr[m][k] = (k & 1) == q ? Sf[m][k >> 1] : Xf[m][k >> 1];
+        }
+    }
 #pragma unroll
     for (int m = 0; m < PPL; ++m) {
         const int j = q + LPE * m;
@@ -1782,7 +1831,7 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
                     gx = px[1] - pxj;
                     gy = py[1] - pyj;
 #else
-                    if constexpr (LPE == 2 && PMAX == 4) {
+                    if constexpr (LPE == 2 && (PMAX == 4 || PMAX == 8)) {
                         // field<double> at planet j from the shared factors:
                         // term k = F(j, k) * (p_k - p_j) summed in k order; the
                         // self term is gm / 1e-12 * (+0), a zero with gm's sign

@@ -21,6 +21,6 @@ step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-m
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 step bench20 300 python bench.py --steps 20 --warmup 5
 step bench1000 300 python bench.py --no-cpu --no-single
-step mb_sector 120 ./tools/mb_sector
-step mb_sector_pmc 120 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d $O/mbpmc -o run -f csv -- ./tools/mb_sector
+step bench_c5 300 python bench.py --workload c5 --no-cpu --no-single
+step bench_c2 300 python bench.py --workload c2 --no-cpu --no-single
 exit 0

@@ -4,6 +4,7 @@
 set -u
 cd "$(dirname "$0")/.."
 OUT=${OUT:-/tmp/astro_isa.s}
+FILTER=${FILTER:-step}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
   -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude --cuda-device-only -S "$@" \
   astro_amd/csrc/astro_kernels.hip -o $OUT 2>/dev/null || exit 1
@@ -12,7 +13,7 @@ import re, sys
 s = open(sys.argv[1]).read()
 for m in re.finditer(r'\.name:\s+(\S+)\n(.*?)\.wavefront_size', s, re.S):
     name, body = m.group(1), m.group(2)
-    if 'step' not in name: continue
+    if FILTER not in name: continue
     f = lambda k: (re.search(r'\.%s:\s+(\d+)' % k, body) or [None, '?'])[1]
     short = re.sub(r'_ZN12_GLOBAL__N_1\d+', '', name).split('EEv')[0]
     print('%-40s vgpr %4s spill %4s sgpr_spill %4s scratch %5s' % (short, f('vgpr_count'), f('vgpr_spill_count'), f('sgpr_spill_count'), f('private_segment_fixed_size')))
