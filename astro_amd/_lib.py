@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libastro_hip.so')
+# (ASTRO_LIB: another build of the same library, e.g. an A/B variant from tools/build_var.sh)
+LIB_PATH = os.environ.get('ASTRO_LIB') or os.path.join(HERE, 'libastro_hip.so')
 ABI_VERSION = 13
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
@@ -16,7 +17,8 @@ STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
 NSTATS = 8
 KERNELS = {'auto': 0, 'lane': 1, 'quad': 2, 'pair': 3}
 ERRORS = {1: 'a helper wave never saw its step wave post (its finished games were not re-created)',
-          2: "a step wave never saw its helper's header read"}
+          2: "a step wave never saw its helper's header read",
+          4: "a step wave never saw its helper's bullet pass"}
 
 
 class AstroParams(ctypes.Structure):

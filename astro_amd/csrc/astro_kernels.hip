@@ -1870,15 +1870,35 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
 
 }
 
+// The pair instance's helpers run the step waves' bullet pass while the step
+// waves run their ships (A/B knob, off: c3 12.13 -> 13.20 us -- the helper's
+// longer path before its resets sets the launch's end;
+// profiles/round3/ab_bullets_on_helper.jsonl)
+#ifndef ASTRO_BULLETS_ON_HELPER
+#define ASTRO_BULLETS_ON_HELPER 0
+#endif
+
 // HELP: each step wave has a helper wave in its workgroup (waves QW..2QW-1)
 // that creates its finished games' next ones.  The step wave posts its
 // finished envs here as soon as it knows them -- before the surviving envs'
 // update -- and goes on; the helper, asleep until then, runs the reset
 // passes meanwhile, so a wave that has a finished game no longer ends a
 // reset pass (~3.9k cycles) after its physics.
+// An LDS word accessed as volatile through the LDS address space: ds_read /
+// ds_write, ordered by lgkmcnt only.  (A volatile access through the plain
+// generic pointer compiles to a flat load/store with sc0 sc1 and an
+// s_waitcnt vmcnt(0): a wait for every global load and store the wave has
+// in flight.)
+typedef volatile __attribute__((address_space(3))) uint32_t lds_vu32;
+__device__ __forceinline__ lds_vu32 *lds_word(const uint32_t &w) {
+    return (lds_vu32 *)size_t(uint32_t(reinterpret_cast<uintptr_t>(&w)));   // a generic LDS address's low half is its offset
+}
+
 struct HelpBox {
     uint32_t flag;                 // set (1) by the step wave once `todo` is written
     uint32_t seen;                 // set (nonzero) by the helper once its header load has returned
+    uint32_t bullets;              // set (1) by the helper once its bullet pass's results are in LDS
+    uint32_t pad;
     unsigned long long todo;       // leader lanes (q == 0) of the finished envs
 };
 
@@ -1890,7 +1910,7 @@ __device__ __forceinline__ void help_post(HelpBox &bx, uint64_t todo, int lane) 
 #endif
     if (lane == 0) bx.todo = todo;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the mask before the flag (LDS: in order per wave)
-    if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.flag) = 1u;
+    if (lane == 0) *lds_word(bx.flag) = 1u;
 }
 
 // A bounded wait for an LDS word another wave of the workgroup sets: true
@@ -1899,10 +1919,10 @@ __device__ __forceinline__ void help_post(HelpBox &bx, uint64_t todo, int lane) 
 // reported through the state's error word (report_error), never ignored.
 __device__ __forceinline__ bool wait_lds_word(const uint32_t &w) {
     for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
-        if (*reinterpret_cast<const volatile uint32_t *>(&w) != 0u) return true;
+        if (*lds_word(w) != 0u) return true;
         __builtin_amdgcn_s_sleep(1);
     }
-    return *reinterpret_cast<const volatile uint32_t *>(&w) != 0u;
+    return *lds_word(w) != 0u;
 }
 
 // Set bits of the state's device error word (AstroState.errors, optional).
@@ -1910,405 +1930,92 @@ __device__ __forceinline__ void report_error(const AstroState &st, uint32_t bits
     if (st.errors && lane == 0) atomicOr(st.errors, bits);
 }
 
-template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false, bool HELP = false,
-          int WPG = QW>
-__device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
-                                                float *__restrict__ reward_all, uint8_t *__restrict__ done_all,
-                                                bool stats, int auto_reset, int kt STAMP_ARG) {
+// ---------------------------------------------------------------------------
+// The dense bullet pass of the quad/pair kernels (core.py:241-251, 264-266,
+// 295-300), in two parts so the first rounds' loads can fly during other
+// work: bullets_begin (after the header) numbers the wave's live bullets --
+// bullet k of env e is g = off_e + k, so the pass runs ceil(sum nb / 64)
+// rounds instead of max over envs of ceil(nb / LPE) -- writes the first
+// index window, clears the envs' LDS words and loads the first two rounds'
+// bullets; bullets_rounds stages the envs' old bodies in LDS, collides,
+// moves, culls and compacts every live bullet, and leaves per env the kept
+// count (s_kept) and the ships the bullets hit (s_hit).  Either the step
+// wave runs both, or (BULLETS_ON_HELPER) its helper wave does, with the same
+// LDS rows, while the step wave runs the ships.
+template <typename T>
+struct BulletsIn {
+    int total, off;
+    uint32_t tag, bw0, bw1;
+    typename Store<T>::V cur0, cur1;
+};
+
+template <typename T, int LPE>
+__device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroState &st, size_t BC, int lane, int e, int q, int base,
+                                                      int nb, int np, bool t0, uint32_t *s_index, int *s_kept,
+                                                      int *s_hit, int *s_serial) {
     using V = typename Store<T>::V;
-    constexpr int PPL = PMAX / LPE;   // planet slots per lane
-    constexpr int QENV = 64 / LPE;    // envs per wave
-    constexpr int NBOD2 = (S + PMAX + 1) / 2;
-    // LDS, one set per wave of the workgroup
-    __shared__ float4 s_body_all[WPG][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
-    __shared__ uint32_t s_index_all[WPG][QWIN];           // a window of the wave's live bullets, see bw_*
-    __shared__ int s_kept_all[WPG][QENV], s_hit_all[WPG][QENV], s_serial_all[WPG][QENV];
-    __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
-    __shared__ HelpBox s_box_all[HELP ? WPG : 1];
-    __shared__ uint32_t s_pre_all[HELP ? WPG : 1][HELP ? QENV : 1][2][13 + 2 * S];   // a helper's chains, made ahead
-    // (wave_sync syncs one wave whenever the build's QW > 1, whatever this instance's WPG)
-    static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, wave-scoped LDS sync");
-    const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
-    const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
-    float4 (*s_body)[NBOD2] = s_body_all[wv];
-    uint32_t *s_index = s_index_all[wv];
-    int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv];
-    uint32_t (*s_chain)[2][13 + 2 * S] = s_chain_all[wv];
-
-    const int N = st.n_env;
-    int lane = threadIdx.x & 63;
-    if constexpr (OPAQUE) asm volatile("" : "+v"(lane));   // (see the rollout kernel)
-    const int q = lane & (LPE - 1);
-    const int e = lane / LPE;
-    const int base = (blockIdx.x * WPG + wv) * QENV;
-    const bool active = base + e < N;     // uniform over the quad
-    const int i = active ? base + e : N - 1;   // spare quads of the last wave shadow env N-1, store nothing
-    const size_t NN = size_t(N);
-    if constexpr (HELP) {
-        // LDS holds the previous launch's leftovers: clear the flag before
-        // any step wave can post (every wave of the workgroup passes this
-        // one barrier; a wave past the last env returns after it, with its
-        // helper)
-        HelpBox &bx = s_box_all[wv];
-        if (helper && lane == 0) {
-            bx.flag = 0;
-            bx.seen = 0;
-            bx.todo = 0;
-        }
-        __syncthreads();
-        if (base >= N) return QuadCounts{};
-        if (helper) {
-            // While its step wave steps, the helper makes the MT19937 init-key
-            // chains of every env's pending game (the first 13 + 2S words from
-            // the seed and from key[397]; 2 lanes per env, all envs at once):
-            // a reset pass then starts from its draws.  A finished env's
-            // header is never written by its step wave, so the helper reads
-            // the same pending seed and key (the step wave's gather of a
-            // first-step env's key repeated here).
-            constexpr int NW = 12 + 2 * S;
-            uint32_t (*pre)[2][13 + 2 * S] = s_pre_all[wv];
-            const int4 hh = reinterpret_cast<const int4 *>(st.hdr)[i];
-            // the step wave stores the survivors' new headers (tick + 1) at
-            // its end: it waits for this word, so the header read here is the
-            // launch's input whatever the memory system's timing (the store
-            // depends on the loaded value: it waits for the load's return)
-            if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&bx.seen) = uint32_t(hh.x) | 1u;
-            const uint32_t hseed = uint32_t(hh.z);
-            const bool kvalid = (uint32_t(hh.x) & KEY_VALID) != 0;
-            uint32_t hkey = uint32_t(hh.w);
-            const bool hk = kvalid || p.key_table != nullptr;
-            if (q == 1 && !kvalid) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
-            // ... and, pair instance, the planet update of every env of the
-            // step wave (the survivors' stored after the post; the step wave
-            // then skips it: c3 12.39 -> 11.92 us with eight step waves per
-            // workgroup; the quad instance of config 2 keeps it, 5.45 vs 5.50)
-            constexpr bool PLANETS = LPE == 2;
-            const size_t NN = size_t(N);
-            V *planets = reinterpret_cast<V *>(st.planets);
-            constexpr int PPL = PMAX / LPE;
-            int np = hh.y & 0xff;
-            np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
-            const bool t0 = (uint32_t(hh.x) & TICK_MASK) == 0;
-            const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
-            V hpv[PPL], hout[PPL];
-            T hpx[PPL], hpy[PPL];
-            if constexpr (PLANETS) {
-#pragma unroll
-                for (int m = 0; m < PPL; ++m) {   // (8 slots: a slot past np aliased to slot 0, as the step wave reads)
-                    const int j = q + LPE * m;
-                    hpv[m] = planets[size_t(j < np ? j : 0) * NN + i];
-                    hpx[m] = hpv[m].x;
-                    hpy[m] = hpv[m].y;
-                }
-            }
-            if (q < 2) {
-                uint32_t x = q == 0 ? hseed : hkey;
-                const uint32_t koff = q == 0 ? 0u : 397u;
-#pragma unroll
-                for (int k = 0; k <= NW; ++k) {
-                    pre[e][q][k] = x;
-                    x = mt_key_next(x, koff + uint32_t(k + 1));
-                }
-            }
-            wave_sync();
-            if constexpr (PLANETS) planet_update<T, S, PMAX, LPE, PPL>(p, hpv, hpx, hpy, q, np, t0, slot_last, hout);
-            // until the step wave posts (bounded: it always posts; if the
-            // bound expires the mask is not trusted -- no stores, no resets --
-            // and the launch reports ASTRO_ERR_HELPER_WAIT)
-            if (!wait_lds_word(bx.flag)) {
-                report_error(st, ASTRO_ERR_HELPER_WAIT, lane);
-                return QuadCounts{};
-            }
-            asm volatile("" ::: "memory");
-#ifdef ASTRO_STAMPS
-            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[20])::"memory");
-#endif
-            QuadCounts hc{};
-            const uint64_t todo0 = bx.todo;
-            if (PLANETS && active && !((todo0 >> (lane & ~(LPE - 1))) & 1ull)) {   // a surviving env: its new planets
-#pragma unroll
-                for (int m = 0; m < PPL; ++m) {
-                    const int j = q + LPE * m;
-                    if (j < np) planets[size_t(j) * NN + i] = hout[m];
-                }
-            }
-            if (todo0) {   // uniform
-                for (uint64_t todo = todo0; todo;)   // uniform
-                    todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, s_chain,
-                                                                  s_serial STAMP_PASS, pre);
-                wave_sync();
-                if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
-                if (active && s_serial[e]) {   // uniform over the quad; rare
-                    const uint32_t kq = uint32_t(quad_bcast_i<1, LPE>(int(hkey)));   // (lane q == 1 has the key)
-                    const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-                    const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, c, stream_ring_of(st, i));
-                    restart_env<T, S, PMAX, LPE>(p, st, i, ng, q);
-                }
-            }
-#ifdef ASTRO_STAMPS
-            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[21])::"memory");
-            stamp_[22] = __popcll(todo0);
-#endif
-            return hc;
-        }
-#if ASTRO_STEP_PRIO > 0
-        // the step wave is the launch's critical path: let it win issue
-        // arbitration over its helper on the shared SIMD
-        __builtin_amdgcn_s_setprio(ASTRO_STEP_PRIO);
-#endif
-    }
-    const size_t BC = size_t(p.b_cap);
-    V *ships = reinterpret_cast<V *>(st.ships);
-    T *ships_b = reinterpret_cast<T *>(st.ships_b);
-    V *planets = reinterpret_cast<V *>(st.planets);
-    V *bullets = reinterpret_cast<V *>(st.bullets);
-    uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;   // per lane, summed over the launch's ticks
-    uint32_t c_reset = 0, c_coll = 0, c_tout = 0, c_serial = 0;           // per wave
-    const int sq = q < S ? q : 0;
-    float *__restrict__ reward = reward_all + size_t(kt) * NN * S;
-    uint8_t *__restrict__ done_out = done_all + size_t(kt) * NN;
-    bool f_reset = false, f_coll = false, f_tout = false;
-    bool need_reset = false;   // leader lane (q == 0) of an env whose game ended, auto-reset on
-    STAMP(0);
-
-    // ---- loads, all independent of each other: header, own ship (lanes <
-    //      S), control, own planet slots (read whether live or not; padding
-    //      is masked below)
-    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
-    const V sv = ships[size_t(sq) * NN + i];
-    const T sbv = ships_b[size_t(sq) * NN + i];
-    int ctl = tick_control<S>(drv, i, sq, NN, kt);
-    V pv[PPL];
-    T mpx[PPL], mpy[PPL];
-    // 4 planet slots: read with the header, every slot (padding is masked
-    // below).  8 slots (config 5: 1-8 planets, 3.5 padded slots per env on
-    // average): read after the header, a slot past the env's planets
-    // aliased to slot 0 -- the line already read, no traffic -- one more
-    // round trip, which three waves per SIMD hide (c5: 56 B less per env,
-    // time unchanged in the A/B)
-    constexpr bool PLANETS_AFTER_HDR = PMAX > 4;
-    // With planets_only (config 3's 3-planet games) a filtered game never
-    // has a planet in the slots past it: those alias slot 0 (the line just
-    // read, no traffic; c3 reads 1 MB less per launch, 12.10 -> 12.03 us
-    // A/B) -- a kernarg bound, so the loads still go out with the header's.
-    // Pair instance with helpers only: the quad instance (c2) lost 2% to the
-    // fallback below, the helper-less pair instance (1M, rollouts) spilled
-    constexpr bool ALIAS = HELP && LPE == 2;
-    const int p_live = ALIAS && p.planets_only ? p.planets_only : p.p_pad;
-    if constexpr (!PLANETS_AFTER_HDR) {
-#pragma unroll
-        for (int m = 0; m < PPL; ++m) {
-            const int j = q + LPE * m;
-            pv[m] = planets[size_t(j < p_live ? j : 0) * NN + i];
-        }
-    }
-    const int tick = int(uint32_t(h.x) & TICK_MASK);
-    const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
-    uint32_t pend_seed = uint32_t(h.z);
-    int np = h.y & 0xff;
-    const int flags = (h.y >> 8) & 0xff;
-    const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
-    np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
-    if constexpr (PLANETS_AFTER_HDR) {
-#pragma unroll
-        for (int m = 0; m < PPL; ++m) {
-            const int j = q + LPE * m;
-            pv[m] = planets[size_t(j < np ? j : 0) * NN + i];
-        }
-    }
-    else if (ALIAS && __builtin_amdgcn_readfirstlane(int(__any(np > p_live))) != 0) {   // uniform; only
-#pragma unroll                                                                         // a loaded state
-        for (int m = 0; m < PPL; ++m) {
-            const int j = q + LPE * m;
-            if (j >= p_live && j < np) pv[m] = planets[size_t(j) * NN + i];
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < PPL; ++m) {
-        mpx[m] = pv[m].x;
-        mpy[m] = pv[m].y;
-    }
-    // does any env of the wave use the last planet slot?  (uniform; with
-    // planets_only < PMAX, e.g. the 3-planet games of config 3, none does
-    // and the float64 fields skip that slot's division)
-    const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
-    const bool live = tick < p.timeout_tick;
-    const bool t0 = tick == 0;
-    STAMP(1);
-    const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
-    uint32_t pend_key = uint32_t(h.w);
-    n_pl += active && q == 0 ? uint32_t(np) : 0u;
-
-    // ---- index the wave's live bullets densely: bullet k of env e is number
-    //      g = off_e + k, so the bullet pass below runs ceil(sum nb / 64)
-    //      rounds instead of max over envs of ceil(nb / 4)
+    const V *bullets = reinterpret_cast<const V *>(st.bullets);
+    BulletsIn<T> b;
     const int incl = wave_incl_scan(q == 0 ? nb : 0, lane);
-    const int off = incl - nb;
+    b.off = incl - nb;
 #ifdef ASTRO_ABLATE_BULLETS   // timing ablation only (wrong results)
-    const int total = 0;
+    b.total = 0;
 #else
-    const int total = __builtin_amdgcn_readlane(incl, 63);
+    b.total = __builtin_amdgcn_readlane(incl, 63);
 #endif
-    const uint32_t tag = bw_tag(e, np, t0);
-    index_window<LPE>(s_index, 0, off, nb, q, tag);
+    b.tag = bw_tag(e, np, t0);
+    index_window<LPE>(s_index, 0, b.off, nb, q, b.tag);
     if (q == 0) {
         s_kept[e] = 0;
         s_hit[e] = 0;
         s_serial[e] = 0;
     }
     wave_sync();
-    // the first two rounds' bullets load during the physics below
-    uint32_t bw0 = lane < total ? s_index[lane] : 0u;
-    uint32_t bw1 = lane + 64 < min(total, QWIN) ? s_index[lane + 64] : 0u;
-    V cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
-    V cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
-    // key[397] of the next game's seed (first step of a game): a random
-    // gather into the 4 GiB key table, issued after every load the physics
-    // waits for, so only its consumers (header store, reset) wait for it
-    if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
-    // stream cursor, for check_pending (read there under this same condition
-    // only).  Every lane loads, the others their own header again (the line
-    // just read: no traffic).  A conditional load made the compiler merge
-    // its value with the other lanes' zeros right after it, i.e. wait for it
-    // -- and for every load before it, the key-table gather included -- at
-    // the top of the wave (c3 13.10 -> 12.65 us, c2 6.74 -> 6.64 us, A/B)
-    const bool want_c = q == 0 && !key_valid && p.key_table && p.planets_only;
-    uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
-    asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // values, not a select between the fields' addresses
-    const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
+    b.bw0 = lane < b.total ? s_index[lane] : 0u;
+    b.bw1 = lane + 64 < min(b.total, QWIN) ? s_index[lane + 64] : 0u;
+    b.cur0 = bullets[size_t(base + bw_env(b.bw0)) * BC + bw_slot(b.bw0)];
+    b.cur1 = bullets[size_t(base + bw_env(b.bw1)) * BC + bw_slot(b.bw1)];
+    return b;
+}
 
-    // ---- quad broadcasts: all planets, both ships
-    double px[PMAX], py[PMAX], sx[S], sy[S];
-    bcast_slots<T, PPL, LPE>(mpx, px);
-    bcast_slots<T, PPL, LPE>(mpy, py);
-    sx[0] = double(quad_bcast<0, LPE>(sv.x));
-    sy[0] = double(quad_bcast<0, LPE>(sv.y));
-    if (S == 2) {
-        sx[S - 1] = double(quad_bcast<S - 1, LPE>(sv.x));
-        sy[S - 1] = double(quad_bcast<S - 1, LPE>(sv.y));
-    }
-
-    // ---- own ship (lanes < S): direction, thrust + gravity (core.py:234-239)
-    const double mx = double(sv.x), my = double(sv.y), mdx = double(sv.z), mdy = double(sv.w);
-    const double mb = double(sbv);
-    if constexpr (BOTS) {   // (the ScriptBot instance) ScriptBot ships decide on the old state
-        if (drv.policy == ASTRO_POLICY_BOTS) {   // uniform
-            double pdx[PMAX], pdy[PMAX];
-            T mpdx[PPL], mpdy[PPL];
-#pragma unroll
-            for (int m = 0; m < PPL; ++m) {
-                mpdx[m] = pv[m].z;
-                mpdy[m] = pv[m].w;
-            }
-            bcast_slots<T, PPL, LPE>(mpdx, pdx);
-            bcast_slots<T, PPL, LPE>(mpdy, pdy);
-            const double d0x = double(quad_bcast<0, LPE>(sv.z)), d0y = double(quad_bcast<0, LPE>(sv.w));
-            const double d1x = double(quad_bcast<S - 1, LPE>(sv.z)), d1y = double(quad_bcast<S - 1, LPE>(sv.w));
-            const int oe = q == 0 ? S - 1 : 0;   // the other ship
-            if (q < S && ship_bot(drv, q) == ASTRO_BOT_SCRIPT)
-                ctl = script_control<S, PMAX>(drv, p.solo != 0, t0, np, px, py, pdx, pdy, mx, my, mdx, mdy, mb,
-                                              sx[oe], sy[oe], oe == 0 ? d0x : d1x, oe == 0 ? d0y : d1y);
-        }
-    }
-    float ds, dc;
-#ifdef ASTRO_ABLATE_SINCOS   // timing ablation only (wrong results)
-    ds = float(mb);
-    dc = float(mx);
-#else
-    np_sincosf(float(mb), ds, dc);
-#endif
-    double ax = 0.0, ay = 0.0;
-    if (q < S) {
-        double gx, gy;
-        if (t0) {
-            float fx, fy;
-            field<float, PMAX>(px, py, np, mx, my, p.gm, fx, fy);
-            gx = double(fx);
-            gy = double(fy);
-        } else {
-#ifdef ASTRO_ABLATE_SHIPFIELD   // timing ablation only (wrong results)
-            gx = px[0] - mx;
-            gy = py[0] - my;
-#else
-            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
-#endif
-        }
-        const double thr = p.thrust * double(ctl & 1);
-        ax = thr * double(ds) + gx;
-        ay = thr * double(dc) + gy;
-    }
-
-    STAMP(2);
-    // ---- ship collisions (core.py:241-253): lane q tests its planets and
-    //      lane 0 the ship pair; quad-OR afterwards
-    const Guard gsp(p.r2_sp), gss(p.r2_ss), gp(p.r2_p0), gs(p.r2_s0);
-    float sxf[S], syf[S], mpxf[PPL], mpyf[PPL];   // float32 copies, padding parked far away
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        sxf[s] = float(sx[s]);
-        syf[s] = float(sy[s]);
-    }
-#pragma unroll
-    for (int m = 0; m < PPL; ++m) {
-        mpxf[m] = q + LPE * m < np ? float(mpx[m]) : -FAR_POS;
-        mpyf[m] = q + LPE * m < np ? float(mpy[m]) : -FAR_POS;
-    }
-    bool hsp[S];
-    {
-        bool amb = false;
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            bool hs = false;
-#pragma unroll
-            for (int m = 0; m < PPL; ++m) hs |= near32_t0(sxf[s], syf[s], mpxf[m], mpyf[m], gsp, amb, t0);
-            hsp[s] = hs;
-        }
-        bool hh = false;
-        if (S == 2 && q == 0) hh = near32_t0(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, amb, t0);
-        if (__any(amb)) {   // the exact tests, for the ambiguous lanes (never tick 0, see near32_t0)
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                bool hs = false;
-#pragma unroll
-                for (int m = 0; m < PPL; ++m)
-                    hs |= (q + LPE * m < np) & closer_exact(sx[s], sy[s], double(mpx[m]), double(mpy[m]), gsp, t0);
-                hsp[s] = amb ? hs : hsp[s];
-            }
-            if (S == 2 && q == 0) hh = amb ? closer_exact(sx[0], sy[0], sx[S - 1], sy[S - 1], gss, t0) : hh;
-        }
-#pragma unroll
-        for (int s = 0; s < S; ++s) hsp[s] = hsp[s] || hh;
-    }
-
+// sxf/syf: both ships' old positions (float32); mpxf/mpyf: the lane's own
+// planet slots q + LPE m (float32, slots past the env's planets parked at
+// -FAR_POS).  Ends with the wave's LDS results readable (wave_sync).
+template <typename T, int S, int PMAX, int LPE>
+__device__ __forceinline__ void bullets_rounds(const AstroParams &p, const AstroState &st, const BulletsIn<T> &b,
+                                               int lane, int e, int q, int base, int nb, const float (&sxf)[S],
+                                               const float (&syf)[S], const float (&mpxf)[PMAX / LPE],
+                                               const float (&mpyf)[PMAX / LPE],
+                                               float4 (*s_body)[(S + PMAX + 1) / 2], uint32_t *s_index,
+                                               int *s_kept, int *s_hit, const Guard &gp, const Guard &gs) {
+    using V = typename Store<T>::V;
+    constexpr int PPL = PMAX / LPE;
+    constexpr int NBOD2 = (S + PMAX + 1) / 2;
+    const size_t NN = size_t(st.n_env);
+    const size_t BC = size_t(p.b_cap);
+    const V *ships = reinterpret_cast<const V *>(st.ships);
+    const V *planets = reinterpret_cast<const V *>(st.planets);
+    V *bullets = reinterpret_cast<V *>(st.bullets);
+    const int total = b.total, off = b.off;
+    const uint32_t tag = b.tag;
+    uint32_t bw0 = b.bw0, bw1 = b.bw1;
+    V cur0 = b.cur0, cur1 = b.cur1;
     // ---- old positions of the env's bodies for the bullet pass (LDS)
     {
         float2 *body = reinterpret_cast<float2 *>(&s_body[e][0]);
-        if (q < S) body[q] = make_float2(q == 0 ? sxf[0] : sxf[S - 1], q == 0 ? syf[0] : syf[S - 1]);
+        // (the ships' values made opaque first: `q == 0 ? a[0] : a[1]` on an
+        // array parameter becomes a[q], an array indexed in scratch memory)
+        float x0 = sxf[0], y0 = syf[0], x1 = sxf[S - 1], y1 = syf[S - 1];
+        asm volatile("" : "+v"(x0), "+v"(y0), "+v"(x1), "+v"(y1));
+        if (q < S) body[q] = make_float2(q == 0 ? x0 : x1, q == 0 ? y0 : y1);
 #pragma unroll
         for (int m = 0; m < PPL; ++m) body[S + q + LPE * m] = make_float2(mpxf[m], mpyf[m]);
     }
     wave_sync();
-
-    // (quad instance only: in the pair instance the extra live range spills)
-    constexpr bool EARLY_POST = HELP && LPE == 4;
-    if constexpr (EARLY_POST) {
-        // a wave without live bullets (every wave of config 2) knows its
-        // finished envs now -- a ship collision or the timeout -- so it
-        // posts them before its bullet pass and output section, not after
-        if (total == 0) {   // uniform
-            bool fin = !live;
-#pragma unroll
-            for (int s = 0; s < S; ++s) fin |= quad_any<LPE>(hsp[s], lane);
-            help_post(s_box_all[wv], __ballot(active && fin && auto_reset && q == 0), lane);
-        }
-    }
-
-    STAMP(3);
-    // ---- bullets (core.py:241-251, 264-266, 295-300): lane g of a round
-    //      takes live bullet r0 + g of the wave: collide with the OLD bodies,
-    //      move, cull, and compact in slot order within its env, in place
-    //      (a bullet is only ever written to a slot <= the one it was read
-    //      from, and every slot is read before any later round writes)
+    // lane g of a round takes live bullet r0 + g of the wave: collide with the
+    // OLD bodies, move, cull, and compact in slot order within its env, in
+    // place (a bullet is only ever written to a slot <= the one it was read
+    // from, and every slot is read before any later round writes)
     {
         const uint64_t lanes_below = (1ull << lane) - 1;
         const double dt = p.dt;
@@ -2488,6 +2195,422 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         }
     }
     wave_sync();
+}
+
+template <typename T, int S, int PMAX, int LPE, bool OPAQUE = false, bool BOTS = false, bool HELP = false,
+          int WPG = QW>
+__device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
+                                                float *__restrict__ reward_all, uint8_t *__restrict__ done_all,
+                                                bool stats, int auto_reset, int kt STAMP_ARG) {
+    using V = typename Store<T>::V;
+    constexpr int PPL = PMAX / LPE;   // planet slots per lane
+    constexpr int QENV = 64 / LPE;    // envs per wave
+    constexpr int NBOD2 = (S + PMAX + 1) / 2;
+    // LDS, one set per wave of the workgroup
+    __shared__ float4 s_body_all[WPG][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
+    __shared__ uint32_t s_index_all[WPG][QWIN];           // a window of the wave's live bullets, see bw_*
+    __shared__ int s_kept_all[WPG][QENV], s_hit_all[WPG][QENV], s_serial_all[WPG][QENV];
+    __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
+    __shared__ HelpBox s_box_all[HELP ? WPG : 1];
+    __shared__ uint32_t s_pre_all[HELP ? WPG : 1][HELP ? QENV : 1][2][13 + 2 * S];   // a helper's chains, made ahead
+    // (wave_sync syncs one wave whenever the build's QW > 1, whatever this instance's WPG)
+    static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, wave-scoped LDS sync");
+    const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
+    const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
+    float4 (*s_body)[NBOD2] = s_body_all[wv];
+    uint32_t *s_index = s_index_all[wv];
+    int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv];
+    uint32_t (*s_chain)[2][13 + 2 * S] = s_chain_all[wv];
+
+    const int N = st.n_env;
+    int lane = threadIdx.x & 63;
+    if constexpr (OPAQUE) asm volatile("" : "+v"(lane));   // (see the rollout kernel)
+    const int q = lane & (LPE - 1);
+    const int e = lane / LPE;
+    const int base = (blockIdx.x * WPG + wv) * QENV;
+    const bool active = base + e < N;     // uniform over the quad
+    const int i = active ? base + e : N - 1;   // spare quads of the last wave shadow env N-1, store nothing
+    const size_t NN = size_t(N);
+    if constexpr (HELP) {
+        // LDS holds the previous launch's leftovers: clear the flag before
+        // any step wave can post (every wave of the workgroup passes this
+        // one barrier; a wave past the last env returns after it, with its
+        // helper)
+        HelpBox &bx = s_box_all[wv];
+        if (helper && lane == 0) {
+            bx.flag = 0;
+            bx.seen = 0;
+            bx.bullets = 0;
+            bx.todo = 0;
+        }
+        __syncthreads();
+        if (base >= N) return QuadCounts{};
+        if (helper) {
+            // While its step wave steps, the helper makes the MT19937 init-key
+            // chains of every env's pending game (the first 13 + 2S words from
+            // the seed and from key[397]; 2 lanes per env, all envs at once):
+            // a reset pass then starts from its draws.  A finished env's
+            // header is never written by its step wave, so the helper reads
+            // the same pending seed and key (the step wave's gather of a
+            // first-step env's key repeated here).
+            constexpr int NW = 12 + 2 * S;
+            uint32_t (*pre)[2][13 + 2 * S] = s_pre_all[wv];
+            const int4 hh = reinterpret_cast<const int4 *>(st.hdr)[i];
+            // the step wave stores the survivors' new headers (tick + 1) at
+            // its end: it waits for this word, so the header read here is the
+            // launch's input whatever the memory system's timing (the store
+            // depends on the loaded value: it waits for the load's return)
+            if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
+            const uint32_t hseed = uint32_t(hh.z);
+            const bool kvalid = (uint32_t(hh.x) & KEY_VALID) != 0;
+            uint32_t hkey = uint32_t(hh.w);
+            const bool hk = kvalid || p.key_table != nullptr;
+            if (q == 1 && !kvalid) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
+            // ... and, pair instance, the planet update of every env of the
+            // step wave (the survivors' stored after the post; the step wave
+            // then skips it: c3 12.39 -> 11.92 us with eight step waves per
+            // workgroup; the quad instance of config 2 keeps it, 5.45 vs 5.50)
+            constexpr bool PLANETS = LPE == 2;
+            const size_t NN = size_t(N);
+            V *planets = reinterpret_cast<V *>(st.planets);
+            constexpr int PPL = PMAX / LPE;
+            int np = hh.y & 0xff;
+            np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+            const bool t0 = (uint32_t(hh.x) & TICK_MASK) == 0;
+            const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
+            V hpv[PPL], hout[PPL];
+            T hpx[PPL], hpy[PPL];
+            if constexpr (PLANETS) {
+#pragma unroll
+                for (int m = 0; m < PPL; ++m) {   // (8 slots: a slot past np aliased to slot 0, as the step wave reads)
+                    const int j = q + LPE * m;
+                    hpv[m] = planets[size_t(j < np ? j : 0) * NN + i];
+                    hpx[m] = hpv[m].x;
+                    hpy[m] = hpv[m].y;
+                }
+            }
+            // ... and, pair instance, the step wave's whole bullet pass
+            // (BULLETS_ON_HELPER, see bullets_begin): the step wave runs its
+            // ships meanwhile and waits for the pass's results (s_kept,
+            // s_hit) only before its rewards.  The bullets' first rounds load
+            // while the chains below are made.
+            constexpr bool BULLETS = LPE == 2 && ASTRO_BULLETS_ON_HELPER;
+            BulletsIn<T> hb{};
+            V hsv{};
+            const int hnb = active ? min(int(uint32_t(hh.y) >> 16), p.b_cap) : 0;
+            if constexpr (BULLETS) {
+                hsv = reinterpret_cast<const V *>(st.ships)[size_t(q < S ? q : 0) * NN + i];
+                hb = bullets_begin<T, LPE>(st, size_t(p.b_cap), lane, e, q, base, hnb, np, t0, s_index, s_kept, s_hit,
+                                           s_serial);
+            }
+            if (q < 2) {
+                uint32_t x = q == 0 ? hseed : hkey;
+                const uint32_t koff = q == 0 ? 0u : 397u;
+#pragma unroll
+                for (int k = 0; k <= NW; ++k) {
+                    pre[e][q][k] = x;
+                    x = mt_key_next(x, koff + uint32_t(k + 1));
+                }
+            }
+            wave_sync();
+            if constexpr (BULLETS) {
+                float sxf[S], syf[S], mpxf[PPL], mpyf[PPL];   // the old bodies (float32), padding far
+                sxf[0] = float(quad_bcast<0, LPE>(hsv.x));
+                syf[0] = float(quad_bcast<0, LPE>(hsv.y));
+                if (S == 2) {
+                    sxf[S - 1] = float(quad_bcast<S - 1, LPE>(hsv.x));
+                    syf[S - 1] = float(quad_bcast<S - 1, LPE>(hsv.y));
+                }
+#pragma unroll
+                for (int m = 0; m < PPL; ++m) {
+                    mpxf[m] = q + LPE * m < np ? float(hpx[m]) : -FAR_POS;
+                    mpyf[m] = q + LPE * m < np ? float(hpy[m]) : -FAR_POS;
+                }
+                const Guard gp(p.r2_p0), gs(p.r2_s0);
+                bullets_rounds<T, S, PMAX, LPE>(p, st, hb, lane, e, q, base, hnb, sxf, syf, mpxf, mpyf, s_body, s_index,
+                                                s_kept, s_hit, gp, gs);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the results before the flag
+                if (lane == 0) *lds_word(bx.bullets) = 1u;
+            }
+            if constexpr (PLANETS) planet_update<T, S, PMAX, LPE, PPL>(p, hpv, hpx, hpy, q, np, t0, slot_last, hout);
+            // until the step wave posts (bounded: it always posts; if the
+            // bound expires the mask is not trusted -- no stores, no resets --
+            // and the launch reports ASTRO_ERR_HELPER_WAIT)
+            if (!wait_lds_word(bx.flag)) {
+                report_error(st, ASTRO_ERR_HELPER_WAIT, lane);
+                return QuadCounts{};
+            }
+            asm volatile("" ::: "memory");
+#ifdef ASTRO_STAMPS
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[20])::"memory");
+#endif
+            QuadCounts hc{};
+            const uint64_t todo0 = bx.todo;
+            if (PLANETS && active && !((todo0 >> (lane & ~(LPE - 1))) & 1ull)) {   // a surviving env: its new planets
+#pragma unroll
+                for (int m = 0; m < PPL; ++m) {
+                    const int j = q + LPE * m;
+                    if (j < np) planets[size_t(j) * NN + i] = hout[m];
+                }
+            }
+            if (todo0) {   // uniform
+                for (uint64_t todo = todo0; todo;)   // uniform
+                    todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, s_chain,
+                                                                  s_serial STAMP_PASS, pre);
+                wave_sync();
+                if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
+                if (active && s_serial[e]) {   // uniform over the quad; rare
+                    const uint32_t kq = uint32_t(quad_bcast_i<1, LPE>(int(hkey)));   // (lane q == 1 has the key)
+                    const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+                    const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, c, stream_ring_of(st, i));
+                    restart_env<T, S, PMAX, LPE>(p, st, i, ng, q);
+                }
+            }
+#ifdef ASTRO_STAMPS
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[21])::"memory");
+            stamp_[22] = __popcll(todo0);
+#endif
+            return hc;
+        }
+#if ASTRO_STEP_PRIO > 0
+        // the step wave is the launch's critical path: let it win issue
+        // arbitration over its helper on the shared SIMD
+        __builtin_amdgcn_s_setprio(ASTRO_STEP_PRIO);
+#endif
+    }
+    const size_t BC = size_t(p.b_cap);
+    V *ships = reinterpret_cast<V *>(st.ships);
+    T *ships_b = reinterpret_cast<T *>(st.ships_b);
+    V *planets = reinterpret_cast<V *>(st.planets);
+    V *bullets = reinterpret_cast<V *>(st.bullets);
+    uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;   // per lane, summed over the launch's ticks
+    uint32_t c_reset = 0, c_coll = 0, c_tout = 0, c_serial = 0;           // per wave
+    const int sq = q < S ? q : 0;
+    float *__restrict__ reward = reward_all + size_t(kt) * NN * S;
+    uint8_t *__restrict__ done_out = done_all + size_t(kt) * NN;
+    bool f_reset = false, f_coll = false, f_tout = false;
+    bool need_reset = false;   // leader lane (q == 0) of an env whose game ended, auto-reset on
+    STAMP(0);
+
+    // ---- loads, all independent of each other: header, own ship (lanes <
+    //      S), control, own planet slots (read whether live or not; padding
+    //      is masked below)
+    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+    const V sv = ships[size_t(sq) * NN + i];
+    const T sbv = ships_b[size_t(sq) * NN + i];
+    int ctl = tick_control<S>(drv, i, sq, NN, kt);
+    V pv[PPL];
+    T mpx[PPL], mpy[PPL];
+    // 4 planet slots: read with the header, every slot (padding is masked
+    // below).  8 slots (config 5: 1-8 planets, 3.5 padded slots per env on
+    // average): read after the header, a slot past the env's planets
+    // aliased to slot 0 -- the line already read, no traffic -- one more
+    // round trip, which three waves per SIMD hide (c5: 56 B less per env,
+    // time unchanged in the A/B)
+    constexpr bool PLANETS_AFTER_HDR = PMAX > 4;
+    // With planets_only (config 3's 3-planet games) a filtered game never
+    // has a planet in the slots past it: those alias slot 0 (the line just
+    // read, no traffic; c3 reads 1 MB less per launch, 12.10 -> 12.03 us
+    // A/B) -- a kernarg bound, so the loads still go out with the header's.
+    // Pair instance with helpers only: the quad instance (c2) lost 2% to the
+    // fallback below, the helper-less pair instance (1M, rollouts) spilled
+    constexpr bool ALIAS = HELP && LPE == 2;
+    const int p_live = ALIAS && p.planets_only ? p.planets_only : p.p_pad;
+    if constexpr (!PLANETS_AFTER_HDR) {
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + LPE * m;
+            pv[m] = planets[size_t(j < p_live ? j : 0) * NN + i];
+        }
+    }
+    const int tick = int(uint32_t(h.x) & TICK_MASK);
+    const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
+    uint32_t pend_seed = uint32_t(h.z);
+    int np = h.y & 0xff;
+    const int flags = (h.y >> 8) & 0xff;
+    const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
+    np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+    if constexpr (PLANETS_AFTER_HDR) {
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + LPE * m;
+            pv[m] = planets[size_t(j < np ? j : 0) * NN + i];
+        }
+    }
+    else if (ALIAS && __builtin_amdgcn_readfirstlane(int(__any(np > p_live))) != 0) {   // uniform; only
+#pragma unroll                                                                         // a loaded state
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + LPE * m;
+            if (j >= p_live && j < np) pv[m] = planets[size_t(j) * NN + i];
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) {
+        mpx[m] = pv[m].x;
+        mpy[m] = pv[m].y;
+    }
+    // does any env of the wave use the last planet slot?  (uniform; with
+    // planets_only < PMAX, e.g. the 3-planet games of config 3, none does
+    // and the float64 fields skip that slot's division)
+    const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
+    const bool live = tick < p.timeout_tick;
+    const bool t0 = tick == 0;
+    STAMP(1);
+    const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
+    uint32_t pend_key = uint32_t(h.w);
+    n_pl += active && q == 0 ? uint32_t(np) : 0u;
+
+    // ---- index the wave's live bullets densely (bullets_begin); their first
+    //      two rounds load during the physics below.  With the bullet pass on
+    //      the helper waves (BULLETS_ON_HELPER) the step wave does none of it
+    constexpr bool BULLETS_ON_HELPER = HELP && LPE == 2 && ASTRO_BULLETS_ON_HELPER;
+    BulletsIn<T> bin{};
+    if constexpr (!BULLETS_ON_HELPER)
+        bin = bullets_begin<T, LPE>(st, BC, lane, e, q, base, nb, np, t0, s_index, s_kept, s_hit, s_serial);
+    const int total = bin.total;
+    // key[397] of the next game's seed (first step of a game): a random
+    // gather into the 4 GiB key table, issued after every load the physics
+    // waits for, so only its consumers (header store, reset) wait for it
+    if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
+    // stream cursor, for check_pending (read there under this same condition
+    // only).  Every lane loads, the others their own header again (the line
+    // just read: no traffic).  A conditional load made the compiler merge
+    // its value with the other lanes' zeros right after it, i.e. wait for it
+    // -- and for every load before it, the key-table gather included -- at
+    // the top of the wave (c3 13.10 -> 12.65 us, c2 6.74 -> 6.64 us, A/B)
+    const bool want_c = q == 0 && !key_valid && p.key_table && p.planets_only;
+    uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
+    asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // values, not a select between the fields' addresses
+    const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
+
+    // ---- quad broadcasts: all planets, both ships
+    double px[PMAX], py[PMAX], sx[S], sy[S];
+    bcast_slots<T, PPL, LPE>(mpx, px);
+    bcast_slots<T, PPL, LPE>(mpy, py);
+    sx[0] = double(quad_bcast<0, LPE>(sv.x));
+    sy[0] = double(quad_bcast<0, LPE>(sv.y));
+    if (S == 2) {
+        sx[S - 1] = double(quad_bcast<S - 1, LPE>(sv.x));
+        sy[S - 1] = double(quad_bcast<S - 1, LPE>(sv.y));
+    }
+
+    // ---- own ship (lanes < S): direction, thrust + gravity (core.py:234-239)
+    const double mx = double(sv.x), my = double(sv.y), mdx = double(sv.z), mdy = double(sv.w);
+    const double mb = double(sbv);
+    if constexpr (BOTS) {   // (the ScriptBot instance) ScriptBot ships decide on the old state
+        if (drv.policy == ASTRO_POLICY_BOTS) {   // uniform
+            double pdx[PMAX], pdy[PMAX];
+            T mpdx[PPL], mpdy[PPL];
+#pragma unroll
+            for (int m = 0; m < PPL; ++m) {
+                mpdx[m] = pv[m].z;
+                mpdy[m] = pv[m].w;
+            }
+            bcast_slots<T, PPL, LPE>(mpdx, pdx);
+            bcast_slots<T, PPL, LPE>(mpdy, pdy);
+            const double d0x = double(quad_bcast<0, LPE>(sv.z)), d0y = double(quad_bcast<0, LPE>(sv.w));
+            const double d1x = double(quad_bcast<S - 1, LPE>(sv.z)), d1y = double(quad_bcast<S - 1, LPE>(sv.w));
+            const int oe = q == 0 ? S - 1 : 0;   // the other ship
+            if (q < S && ship_bot(drv, q) == ASTRO_BOT_SCRIPT)
+                ctl = script_control<S, PMAX>(drv, p.solo != 0, t0, np, px, py, pdx, pdy, mx, my, mdx, mdy, mb,
+                                              sx[oe], sy[oe], oe == 0 ? d0x : d1x, oe == 0 ? d0y : d1y);
+        }
+    }
+    float ds, dc;
+#ifdef ASTRO_ABLATE_SINCOS   // timing ablation only (wrong results)
+    ds = float(mb);
+    dc = float(mx);
+#else
+    np_sincosf(float(mb), ds, dc);
+#endif
+    double ax = 0.0, ay = 0.0;
+    if (q < S) {
+        double gx, gy;
+        if (t0) {
+            float fx, fy;
+            field<float, PMAX>(px, py, np, mx, my, p.gm, fx, fy);
+            gx = double(fx);
+            gy = double(fy);
+        } else {
+#ifdef ASTRO_ABLATE_SHIPFIELD   // timing ablation only (wrong results)
+            gx = px[0] - mx;
+            gy = py[0] - my;
+#else
+            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
+#endif
+        }
+        const double thr = p.thrust * double(ctl & 1);
+        ax = thr * double(ds) + gx;
+        ay = thr * double(dc) + gy;
+    }
+
+    STAMP(2);
+    // ---- ship collisions (core.py:241-253): lane q tests its planets and
+    //      lane 0 the ship pair; quad-OR afterwards
+    const Guard gsp(p.r2_sp), gss(p.r2_ss), gp(p.r2_p0), gs(p.r2_s0);
+    float sxf[S], syf[S], mpxf[PPL], mpyf[PPL];   // float32 copies, padding parked far away
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        sxf[s] = float(sx[s]);
+        syf[s] = float(sy[s]);
+    }
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) {
+        mpxf[m] = q + LPE * m < np ? float(mpx[m]) : -FAR_POS;
+        mpyf[m] = q + LPE * m < np ? float(mpy[m]) : -FAR_POS;
+    }
+    bool hsp[S];
+    {
+        bool amb = false;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            bool hs = false;
+#pragma unroll
+            for (int m = 0; m < PPL; ++m) hs |= near32_t0(sxf[s], syf[s], mpxf[m], mpyf[m], gsp, amb, t0);
+            hsp[s] = hs;
+        }
+        bool hh = false;
+        if (S == 2 && q == 0) hh = near32_t0(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, amb, t0);
+        if (__any(amb)) {   // the exact tests, for the ambiguous lanes (never tick 0, see near32_t0)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                bool hs = false;
+#pragma unroll
+                for (int m = 0; m < PPL; ++m)
+                    hs |= (q + LPE * m < np) & closer_exact(sx[s], sy[s], double(mpx[m]), double(mpy[m]), gsp, t0);
+                hsp[s] = amb ? hs : hsp[s];
+            }
+            if (S == 2 && q == 0) hh = amb ? closer_exact(sx[0], sy[0], sx[S - 1], sy[S - 1], gss, t0) : hh;
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) hsp[s] = hsp[s] || hh;
+    }
+
+    // (quad instance only: in the pair instance the extra live range spills)
+    constexpr bool EARLY_POST = HELP && LPE == 4;
+    if constexpr (EARLY_POST) {
+        // a wave without live bullets (every wave of config 2) knows its
+        // finished envs now -- a ship collision or the timeout -- so it
+        // posts them before its bullet pass and output section, not after
+        if (total == 0) {   // uniform
+            bool fin = !live;
+#pragma unroll
+            for (int s = 0; s < S; ++s) fin |= quad_any<LPE>(hsp[s], lane);
+            help_post(s_box_all[wv], __ballot(active && fin && auto_reset && q == 0), lane);
+        }
+    }
+
+    STAMP(3);
+    // ---- bullets (core.py:241-251, 264-266, 295-300): collide with the old
+    //      bodies, move, cull, compact in place (bullets_rounds) -- here, or,
+    //      with BULLETS_ON_HELPER, on the helper wave while this wave ran its
+    //      ships: then wait for its results (s_kept, s_hit)
+    if constexpr (!BULLETS_ON_HELPER) {
+        bullets_rounds<T, S, PMAX, LPE>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf, s_body, s_index,
+                                        s_kept, s_hit, gp, gs);
+    } else {
+        if (!wait_lds_word(s_box_all[wv].bullets)) report_error(st, ASTRO_ERR_BULLETS_WAIT, lane);
+    }
     if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
         if (!wait_lds_word(s_box_all[wv].seen)) report_error(st, ASTRO_ERR_HEADER_WAIT, lane);
     }

@@ -251,9 +251,8 @@ def main():
                     help='secondary line: the workload as K-tick rollouts with the on-device random '
                          'policy, K ticks per launch (0 = skip)')
     ap.add_argument('--no-features', action='store_true', help='skip the observation-builder line')
-    ap.add_argument('--eager-head', type=int, default=2,
-                    help='timed launches issued eagerly before the graph replays (the GPU runs them while '
-                         'the host submits the first graph, so it never idles at the start of the region)')
+    ap.add_argument('--eager-head', type=int, default=0,
+                    help='timed launches issued eagerly before the graph replays (0: all in graphs)')
     ap.add_argument('--no-single', action='store_true', help='skip the single-game drop-in latency line')
     ap.add_argument('--stub', action='store_true', help=argparse.SUPPRESS)   # launcher test: no GPU work
     args = ap.parse_args()
@@ -317,17 +316,32 @@ def main():
     # per-launch cost is out of the loop and the GPU runs the eager head while
     # the host submits the first graph.  Each graph is replayed once, untimed,
     # before the region: its first replay uploads it.
+    # The K launches' own GPU time is bracketed by two events recorded INSIDE
+    # the graphs (event-record nodes: before the first launch of the first
+    # graph, after the last launch of the last), so it excludes the host's
+    # graph submission; the stream events around the replays include it.
     head = min(args.steps, max(0, args.eager_head)) if args.graph > 0 else args.steps
     graphs = []
+    in_graph = None
     if args.graph > 0 and head < args.steps:
+        starts = list(range(head, args.steps, args.graph))
+        try:
+            in_graph = (torch.cuda.Event(enable_timing=True, external=True),
+                        torch.cuda.Event(enable_timing=True, external=True))
+        except TypeError:   # (a torch without external events)
+            in_graph = None
         cap = torch.cuda.Stream(dev)
         cap.wait_stream(stream)
         with torch.cuda.stream(cap):
-            for g0 in range(head, args.steps, args.graph):
+            for gi, g0 in enumerate(starts):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cap):
+                    if in_graph and gi == 0:
+                        in_graph[0].record(cap)
                     for k in range(g0, min(args.steps, g0 + args.graph)):
                         env.launch(ptrs[args.warmup + k])
+                    if in_graph and gi == len(starts) - 1:
+                        in_graph[1].record(cap)
                 graphs.append(g)
         stream.wait_stream(cap)
         for g in graphs:
@@ -347,7 +361,15 @@ def main():
     wall = time.perf_counter() - t0
     barrier()
     s1 = env.stat_dict()
-    gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
+    gpu_ms_stream = ev0.elapsed_time(ev1) / args.steps
+    gpu_ms_per_step, gpu_timing = gpu_ms_stream, 'hipEvent pair on the stream around the timed region / K'
+    if in_graph and head == 0:
+        try:
+            gpu_ms_per_step = in_graph[0].elapsed_time(in_graph[1]) / args.steps
+            gpu_timing = ('hipEvent record nodes inside the captured graphs, before the first and after the last of '
+                          'the K launches / K')
+        except RuntimeError:
+            pass
     dev_err = env.device_errors()
 
     # Kernel duration: launches timed one by one (hipEvent pair around each,
@@ -418,9 +440,10 @@ def main():
     if rank == 0:
         n_total = n * world
         value = n_total * args.steps / wall_max
-        # per-launch duration = hipEvents bracketing the timed region (the
-        # hipGraph replays) / K; rocprofv3's kernel average agrees within ~2%
-        # (profiles/round1); one event pair per eager launch adds ~2.5 us
+        # per-launch duration = the K launches' GPU time / K (event-record
+        # nodes inside the graphs: kernels plus the gaps between them, not the
+        # host's submission); rocprofv3's kernel average is compared with it
+        # in profiles/; one event pair per eager launch adds ~2.5 us
         launch_ms = gpu_ms_per_step
         achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
         # PMC-measured HBM bytes and VALU instructions per launch come from
@@ -489,9 +512,9 @@ def main():
                           kernel_ms_eager_event_pairs=kern_ms,
                           kernel=('astro_step_kernel' if env.step_kernel == 'lane' else 'astro_step_quad_kernel'),
                           lanes_per_env=dict(lane=1, quad=4, pair=2)[env.step_kernel],
-                          timing='hipEvent pair around the timed region / K launches'),
+                          timing=gpu_timing),
             issue_roofline=issue,
-            gpu_ms_per_step=gpu_ms_per_step,
+            gpu_ms_per_step=gpu_ms_per_step, gpu_ms_per_step_stream_events=gpu_ms_stream,
             timed_region='%d launches: %d eager, then %s' % (
                 args.steps, head, ('%d hipGraph replay(s) of up to %d launches, each graph replayed once '
                                    'untimed before the region' % (len(graphs), args.graph)) if graphs else 'no graph'),

@@ -122,7 +122,8 @@ typedef struct AstroState {
 enum {
     ASTRO_ERR_HELPER_WAIT = 1,  /* a helper wave's wait for its step wave's post expired:
                                    that wave's finished games were not re-created */
-    ASTRO_ERR_HEADER_WAIT = 2   /* a step wave's wait for its helper's header read expired */
+    ASTRO_ERR_HEADER_WAIT = 2,  /* a step wave's wait for its helper's header read expired */
+    ASTRO_ERR_BULLETS_WAIT = 4  /* a step wave's wait for its helper's bullet pass expired */
 };
 
 /* Control sources of astro_rollout / astro_controls. */

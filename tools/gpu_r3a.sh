@@ -21,6 +21,8 @@ step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-m
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 step bench20 300 python bench.py --steps 20 --warmup 5
 step bench1000 300 python bench.py --no-cpu --no-single
+step ab_c3 300 python tools/ab.py --libs libastro_hip_sym8,libastro_hip_hbul --workload c3 --rounds 5
+step ab_c5 300 python tools/ab.py --libs libastro_hip_sym8,libastro_hip_hbul --workload c5 --rounds 3
 step bench_c5 300 python bench.py --workload c5 --no-cpu --no-single
 step bench_c2 300 python bench.py --workload c2 --no-cpu --no-single
 exit 0

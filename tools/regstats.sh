@@ -4,12 +4,13 @@
 set -u
 cd "$(dirname "$0")/.."
 OUT=${OUT:-/tmp/astro_isa.s}
-FILTER=${FILTER:-step}
+export FILTER=${FILTER:-step}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
   -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude --cuda-device-only -S "$@" \
-  astro_amd/csrc/astro_kernels.hip -o $OUT 2>/dev/null || exit 1
+  ${SRC:-astro_amd/csrc/astro_kernels.hip} -o $OUT 2>/dev/null || exit 1
 python3 - "$OUT" <<'PY'
-import re, sys
+import os, re, sys
+FILTER = os.environ.get('FILTER', 'step')
 s = open(sys.argv[1]).read()
 for m in re.finditer(r'\.name:\s+(\S+)\n(.*?)\.wavefront_size', s, re.S):
     name, body = m.group(1), m.group(2)
