@@ -9,8 +9,9 @@ the reference bit for bit (tests/test_gpu_parity.py): inputs are never
 mutated, a finished game returns ``(None, reward)`` with an int64 reward for
 a collision and a float32 reward for a timeout.
 
-This path is latency-bound by design: per tick one H2D copy of the packed
-state, one tiny launch, one D2H copy and a synchronisation (``_Shim``);
+This path is latency-bound by design: the game's arrays live in host memory
+the kernel addresses directly (``_MappedArena``, C-ABI astro_host_alloc), so
+a tick is one tiny launch and one synchronisation, no copies (``_Shim``);
 bulk simulation belongs on :class:`astro_amd.env.BatchedEnv`.
 """
 import ctypes
@@ -30,21 +31,59 @@ def _device():
     return torch.device('cuda', torch.cuda.current_device())
 
 
+class _MappedArena:
+    """The arrays of one game packed (16-byte aligned) into page-locked host
+    memory that the kernels address directly (astro_host_alloc): numpy
+    views for the host, device addresses for AstroState.  No copies: a
+    kernel's loads and stores cross PCIe."""
+
+    def __init__(self, lib, specs):
+        self.lib = lib
+        self.layout = {}
+        off = 0
+        for name, shape, dt in specs:
+            nbytes = int(np.prod(shape)) * np.dtype(dt).itemsize
+            self.layout[name] = (off, shape, dt, nbytes)
+            off = (off + nbytes + 15) // 16 * 16
+        self.nbytes = off
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(lib.astro_host_alloc(off, ctypes.byref(h), ctypes.byref(d)), 'astro_host_alloc')
+        self.host, self.device = h.value, d.value
+        raw = np.frombuffer((ctypes.c_uint8 * off).from_address(self.host), dtype=np.uint8)
+        raw[:] = 0
+        self.views = {n: raw[o:o + nb].view(dt).reshape(shape) for n, (o, shape, dt, nb) in self.layout.items()}
+
+    def ptr(self, name):
+        return self.device + self.layout[name][0]
+
+    def __del__(self):
+        if getattr(self, 'host', None):
+            self.lib.astro_host_free(ctypes.c_void_p(self.host))
+            self.host = None
+
+
 class _Shim:
     """One float64 game on the device for the single-game surface.  Its
-    state arrays live in ONE device buffer mirrored by one pinned host
-    buffer (BatchedEnv(arena=True)): a tick is one H2D copy of the input
-    (header, ships, planets, bullets, control, fire word), one launch, one
-    D2H copy of everything back, one synchronisation."""
+    state lives in host memory the kernel addresses directly (_MappedArena):
+    a tick writes the input into it, launches, synchronises and reads the
+    result -- one launch and one synchronisation, no copies."""
 
     def __init__(self, config, b_cap, device):
         self.env = env = BatchedEnv(config, 1, device=device, b_cap=b_cap, dtype=torch.float64,
-                                    auto_reset=False, use_key_table=False, arena=True)
-        self.S = env.S
-        a = env.arena
-        self.h = {k: a.host_view(k) for k in a.layout}
-        self.in_bytes = a.end('fire')      # hdr .. fire: a tick's input
-        self.ctl_ptr = a.dev_view('control').data_ptr()
+                                    auto_reset=False, use_key_table=False)
+        S, P = env.S, env.p_pad
+        f8, i4 = np.float64, np.int32
+        self.arena = a = _MappedArena(env.lib, (
+            ('hdr', (1, 4), i4), ('ships', (S, 1, 4), f8), ('ships_b', (S, 1), f8), ('planets', (P, 1, 4), f8),
+            ('bullets', (1, b_cap, 4), f8), ('control', (1, S), np.int8), ('fire', (2,), i4),
+            ('reward', (1, S), np.float32), ('done', (1,), np.uint8), ('seed', (1,), np.uint32)))
+        self.h = a.views
+        # the env's own state record with its arrays moved to the mapped memory
+        # (its seed stream, error word and schedule stay the BatchedEnv's)
+        st = env.state
+        self.state = type(st)(ships=a.ptr('ships'), ships_b=a.ptr('ships_b'), planets=a.ptr('planets'),
+                              bullets=a.ptr('bullets'), hdr=a.ptr('hdr'), stream=st.stream,
+                              stream_ring=st.stream_ring, n_env=1, state_f64=1, errors=st.errors)
         # the launch's schedule per (first tick of a game?, times out?):
         # fire word = arena 'fire', timeout tick so `timeout` holds this call
         self.params = {}
@@ -52,12 +91,24 @@ class _Shim:
             for to in (False, True):
                 p = type(env.params).from_buffer_copy(env.params)
                 p.timeout_tick = tick if to else tick + 1
-                p.fire_bits = a.dev_view('fire').data_ptr()
+                p.fire_bits = a.ptr('fire')
                 self.params[tick, to] = p
-        self.stream = None
 
-    def state(self):
-        """Reference-shaped State from the host mirror (after a pull)."""
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.env.device).cuda_stream)
+
+    def sync(self):
+        torch.cuda.current_stream(self.env.device).synchronize()
+        self.env.check_errors()
+
+    def create(self, seed):
+        self.h['seed'][0] = seed
+        _lib.check(self.env.lib.astro_reset(ctypes.byref(self.env.params), ctypes.byref(self.state),
+                                            self.arena.ptr('seed'), None, self.stream()), 'astro_reset')
+        self.sync()
+
+    def state_of(self):
+        """Reference-shaped State from the mapped arrays."""
         h = self.h
         hdr = h['hdr'].view(np.uint32)
         host = dict(ships=h['ships'].transpose(1, 0, 2), ships_b=h['ships_b'].transpose(1, 0),
@@ -65,12 +116,6 @@ class _Shim:
                     tick=hdr[:, 0] & 0x3fffff, nplanets=hdr[:, 1] & 0xff, nbullets=(hdr[:, 1] >> 16) & 0xffff,
                     flags=(hdr[:, 1] >> 8) & 0xff)
         return self.env.state_of(0, host)
-
-    def sync_pull(self):
-        self.env.arena.pull()
-        torch.cuda.current_stream(self.env.device).synchronize()
-        if self.h['errors'][0]:
-            self.env.check_errors()
 
 
 def _shim(config, bullets_needed):
@@ -91,9 +136,8 @@ def create(config):
     if not 0 <= seed < 1 << 32:   # as np.random.RandomState(seed) (core.py:89) refuses it
         raise ValueError('Seed must be between 0 and 2**32 - 1')
     sh = _shim(config, 0)
-    sh.env.reset(seeds=[seed])
-    sh.sync_pull()
-    return sh.state()
+    sh.create(seed)
+    return sh.state_of()
 
 
 def step(state, control, config):
@@ -116,7 +160,7 @@ def step(state, control, config):
     npl = state.planets.x.shape[0]
     if npl > env.p_pad:
         raise ValueError('a state holds more planets than max_planets')
-    # the input, written into the pinned mirror and sent in one copy
+    # the input, written straight into the memory the kernel reads
     hdr = h['hdr'].view(np.uint32)
     hdr[0, 0] = (int(hdr[0, 0]) & ~0x3fffff & 0xffffffff) | tick
     hdr[0, 1] = npl | (nb << 16)
@@ -131,20 +175,19 @@ def step(state, control, config):
         h['bullets'][0, :nb, 2:4] = state.bullets.dx
     h['control'][0] = control
     h['fire'][0] = int(fire) << tick
-    env.arena.push(sh.in_bytes)
-    rc = env.lib.astro_step(ctypes.byref(sh.params[tick, bool(timeout)]), ctypes.byref(env.state), sh.ctl_ptr,
-                            env.reward.data_ptr(), env.done.data_ptr(), None, 0,
-                            ctypes.c_void_p(torch.cuda.current_stream(env.device).cuda_stream))
+    a = sh.arena
+    rc = env.lib.astro_step(ctypes.byref(sh.params[tick, bool(timeout)]), ctypes.byref(sh.state), a.ptr('control'),
+                            a.ptr('reward'), a.ptr('done'), None, 0, sh.stream())
     if rc != 0:
         _lib.check(rc, 'astro_step')
-    sh.sync_pull()
+    sh.sync()
     done = int(h['done'][0])
     reward = h['reward'][0].copy()
     if done == 1:
         return None, reward.astype(np.int64)
     if done == 2:
         return None, reward.astype(np.float32)
-    nxt = sh.state()
+    nxt = sh.state_of()
     reload = state.reload + config.dt
     if fire:
         reload -= config.reload_time

@@ -1870,6 +1870,12 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
 
 }
 
+// The step wave waits for its helper's header read (HelpBox.seen) before it
+// rewrites the headers (A/B knob)
+#ifndef ASTRO_HDR_HANDSHAKE
+#define ASTRO_HDR_HANDSHAKE 1
+#endif
+
 // The pair instance's helpers run the step waves' bullet pass while the step
 // waves run their ships (A/B knob, off: c3 12.13 -> 13.20 us -- the helper's
 // longer path before its resets sets the launch's end;
@@ -1987,7 +1993,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
                                                const float (&syf)[S], const float (&mpxf)[PMAX / LPE],
                                                const float (&mpyf)[PMAX / LPE],
                                                float4 (*s_body)[(S + PMAX + 1) / 2], uint32_t *s_index,
-                                               int *s_kept, int *s_hit, const Guard &gp, const Guard &gs) {
+                                               int *s_kept, int *s_hit, const Guard &gp, const Guard &gs STAMP_ARG) {
     using V = typename Store<T>::V;
     constexpr int PPL = PMAX / LPE;
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
@@ -2012,6 +2018,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
         for (int m = 0; m < PPL; ++m) body[S + q + LPE * m] = make_float2(mpxf[m], mpyf[m]);
     }
     wave_sync();
+    STAMP(16);
     // lane g of a round takes live bullet r0 + g of the wave: collide with the
     // OLD bodies, move, cull, and compact in slot order within its env, in
     // place (a bullet is only ever written to a slot <= the one it was read
@@ -2186,6 +2193,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           } else {
               rounds(std::integral_constant<int, 1>(), w0, bws, curs);
           }
+          STAMP(17);
           if (nr >= 3) rounds(std::integral_constant<int, 1>(), w0 + 128, bws + 2, curs + 2);
           for (int r0 = w0 + 192; r0 < wend; r0 += 64) {   // uniform; rare
               const uint32_t bw = r0 + lane < wend ? s_index[r0 + lane - w0] : 0u;
@@ -2328,7 +2336,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 }
                 const Guard gp(p.r2_p0), gs(p.r2_s0);
                 bullets_rounds<T, S, PMAX, LPE>(p, st, hb, lane, e, q, base, hnb, sxf, syf, mpxf, mpyf, s_body, s_index,
-                                                s_kept, s_hit, gp, gs);
+                                                s_kept, s_hit, gp, gs STAMP_PASS);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the results before the flag
                 if (lane == 0) *lds_word(bx.bullets) = 1u;
             }
@@ -2468,6 +2476,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     if constexpr (!BULLETS_ON_HELPER)
         bin = bullets_begin<T, LPE>(st, BC, lane, e, q, base, nb, np, t0, s_index, s_kept, s_hit, s_serial);
     const int total = bin.total;
+    STAMP(19);
     // key[397] of the next game's seed (first step of a game): a random
     // gather into the 4 GiB key table, issued after every load the physics
     // waits for, so only its consumers (header store, reset) wait for it
@@ -2607,11 +2616,11 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     //      ships: then wait for its results (s_kept, s_hit)
     if constexpr (!BULLETS_ON_HELPER) {
         bullets_rounds<T, S, PMAX, LPE>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf, s_body, s_index,
-                                        s_kept, s_hit, gp, gs);
+                                        s_kept, s_hit, gp, gs STAMP_PASS);
     } else {
         if (!wait_lds_word(s_box_all[wv].bullets)) report_error(st, ASTRO_ERR_BULLETS_WAIT, lane);
     }
-    if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
+    if constexpr (HELP && ASTRO_HDR_HANDSHAKE) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
         if (!wait_lds_word(s_box_all[wv].seen)) report_error(st, ASTRO_ERR_HEADER_WAIT, lane);
     }
     const int wr_in = s_kept[e];
@@ -3383,6 +3392,31 @@ int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *s
     hipLaunchKernelGGL(astro_stream_init_kernel, dim3(grid), dim3(BLOCK), 0,
                        reinterpret_cast<hipStream_t>(stream), *s, stream_seeds);
     return launched("astro_stream_init");
+}
+
+int astro_host_alloc(uint64_t bytes, void **host, void **device) {
+    if (!host || !device) return fail(-80, "host/device is NULL");
+    *host = *device = nullptr;
+    if (bytes == 0) return fail(-81, "bytes must be > 0");
+    void *h = nullptr;
+    hipError_t e = hipHostMalloc(&h, size_t(bytes), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return fail(-1000 - int(e), "hipHostMalloc(%llu) failed: %s", (unsigned long long)bytes,
+                                     hipGetErrorString(e));
+    void *d = nullptr;
+    e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(h);
+        return fail(-1000 - int(e), "hipHostGetDevicePointer failed: %s", hipGetErrorString(e));
+    }
+    *host = h;
+    *device = d;
+    return 0;
+}
+
+int astro_host_free(void *host) {
+    if (!host) return 0;
+    const hipError_t e = hipHostFree(host);
+    return e == hipSuccess ? 0 : fail(-1000 - int(e), "hipHostFree failed: %s", hipGetErrorString(e));
 }
 
 int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_t rows, void *stream) {

@@ -69,47 +69,6 @@ def key_table(device):
 QUAD_MAX_ENVS = 32768   # include/astro_step.h ASTRO_QUAD_MAX_ENVS
 
 
-class _Arena:
-    """Named arrays packed (16-byte aligned) into one device buffer, with a
-    pinned host mirror and numpy views of it: one H2D and one D2H copy move
-    them all."""
-
-    def __init__(self, specs, device):
-        self.layout = {}
-        off = 0
-        for name, shape, dt in specs:
-            nbytes = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
-            self.layout[name] = (off, shape, dt, nbytes)
-            off = (off + nbytes + 15) // 16 * 16
-        self.nbytes = off
-        self.dev = torch.zeros(off, dtype=torch.uint8, device=device)
-        self.host = torch.zeros(off, dtype=torch.uint8).pin_memory()
-        self.np = self.host.numpy()
-
-    def _view(self, buf, name):
-        off, shape, dt, nbytes = self.layout[name]
-        return buf[off:off + nbytes].view(dt).view(shape)
-
-    def dev_view(self, name):
-        return self._view(self.dev, name)
-
-    def host_view(self, name):
-        """numpy view of the pinned mirror (writes go out with push())."""
-        return self._view(self.host, name).numpy()
-
-    def end(self, name):
-        off, _, _, nbytes = self.layout[name]
-        return off + nbytes
-
-    def push(self, upto):
-        """Host mirror -> device, bytes [0, upto) (stream-ordered, async)."""
-        self.dev[:upto].copy_(self.host[:upto], non_blocking=True)
-
-    def pull(self):
-        """Device -> host mirror, every byte (stream-ordered, async)."""
-        self.host.copy_(self.dev, non_blocking=True)
-
-
 class BatchedEnv:
     """N lockstep games of one Config on one device.
 
@@ -132,7 +91,7 @@ class BatchedEnv:
 
     def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
                  dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto',
-                 use_key_table=True, planets_only=0, arena=False):
+                 use_key_table=True, planets_only=0):
         _schedule.check_config(config)
         planets_only = int(planets_only)
         if planets_only and (not 1 <= planets_only <= config.max_planets
@@ -159,22 +118,17 @@ class BatchedEnv:
 
         N, S, dev = self.n_env, self.S, self.device
         z = lambda *shape, dt=dtype: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
-        # the arrays a tick reads and writes; with arena=True they are views of
-        # ONE device buffer mirrored by one pinned host buffer, so a host that
-        # owns the state (the single-game shim, astro_amd.core) moves a tick's
-        # input and output with one copy each way
-        specs = (('hdr', (N, 4), torch.int32), ('ships', (S, N, 4), dtype), ('ships_b', (S, N), dtype),
-                 ('planets', (self.p_pad, N, 4), dtype), ('bullets', (N, self.b_cap, 4), dtype),
-                 ('control', (N, S), torch.int8), ('fire', (2,), torch.int32),
-                 ('reward', (N, S), torch.float32), ('done', (N,), torch.uint8), ('errors', (1,), torch.int32))
-        self.arena = _Arena(specs, dev) if arena else None
-        for name, shape, dt in specs:
-            if name not in ('control', 'fire'):
-                setattr(self, name, self.arena.dev_view(name) if arena else z(*shape, dt=dt))
+        self.ships = z(S, N, 4)
+        self.ships_b = z(S, N)
+        self.planets = z(self.p_pad, N, 4)
+        self.bullets = z(N, self.b_cap, 4)
+        self.hdr = z(N, 4, dt=torch.int32)
+        self.reward = z(N, S, dt=torch.float32)
+        self.done = z(N, dt=torch.uint8)
+        self.errors = z(1, dt=torch.int32)   # AstroState.errors: the ASTRO_ERR_* bits a faulting launch sets
         self.stream = z(N, 4, dt=torch.int32)
         self.stream_ring = z(N, MT_N, dt=torch.int32)
         self.stats = z(max(1, (N + 15) // 16), _lib.NSTATS, dt=torch.int64)
-        # (errors: AstroState.errors, the ASTRO_ERR_* bits a faulting launch sets)
         self.fire_bits = torch.from_numpy(self.schedule.fire_bits().view(np.int32)).to(dev)
 
         k = _schedule.kernel_constants(config)

@@ -251,8 +251,9 @@ def main():
                     help='secondary line: the workload as K-tick rollouts with the on-device random '
                          'policy, K ticks per launch (0 = skip)')
     ap.add_argument('--no-features', action='store_true', help='skip the observation-builder line')
-    ap.add_argument('--eager-head', type=int, default=0,
-                    help='timed launches issued eagerly before the graph replays (0: all in graphs)')
+    ap.add_argument('--eager-head', type=int, default=4,
+                    help='timed launches issued eagerly before the graph replays: the GPU runs them while the '
+                         'host submits the first graph (~10-40 us), so it does not idle at the start of the region')
     ap.add_argument('--no-single', action='store_true', help='skip the single-game drop-in latency line')
     ap.add_argument('--stub', action='store_true', help=argparse.SUPPRESS)   # launcher test: no GPU work
     args = ap.parse_args()
@@ -316,32 +317,17 @@ def main():
     # per-launch cost is out of the loop and the GPU runs the eager head while
     # the host submits the first graph.  Each graph is replayed once, untimed,
     # before the region: its first replay uploads it.
-    # The K launches' own GPU time is bracketed by two events recorded INSIDE
-    # the graphs (event-record nodes: before the first launch of the first
-    # graph, after the last launch of the last), so it excludes the host's
-    # graph submission; the stream events around the replays include it.
     head = min(args.steps, max(0, args.eager_head)) if args.graph > 0 else args.steps
     graphs = []
-    in_graph = None
     if args.graph > 0 and head < args.steps:
-        starts = list(range(head, args.steps, args.graph))
-        try:
-            in_graph = (torch.cuda.Event(enable_timing=True, external=True),
-                        torch.cuda.Event(enable_timing=True, external=True))
-        except TypeError:   # (a torch without external events)
-            in_graph = None
         cap = torch.cuda.Stream(dev)
         cap.wait_stream(stream)
         with torch.cuda.stream(cap):
-            for gi, g0 in enumerate(starts):
+            for g0 in range(head, args.steps, args.graph):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cap):
-                    if in_graph and gi == 0:
-                        in_graph[0].record(cap)
                     for k in range(g0, min(args.steps, g0 + args.graph)):
                         env.launch(ptrs[args.warmup + k])
-                    if in_graph and gi == len(starts) - 1:
-                        in_graph[1].record(cap)
                 graphs.append(g)
         stream.wait_stream(cap)
         for g in graphs:
@@ -357,19 +343,30 @@ def main():
     for g in graphs:
         g.replay()
     ev1.record(stream)
+    while not ev1.query():   # (busy-poll the end: a blocking wait wakes ~10 us late)
+        pass
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     barrier()
     s1 = env.stat_dict()
     gpu_ms_stream = ev0.elapsed_time(ev1) / args.steps
     gpu_ms_per_step, gpu_timing = gpu_ms_stream, 'hipEvent pair on the stream around the timed region / K'
-    if in_graph and head == 0:
-        try:
-            gpu_ms_per_step = in_graph[0].elapsed_time(in_graph[1]) / args.steps
-            gpu_timing = ('hipEvent record nodes inside the captured graphs, before the first and after the last of '
-                          'the K launches / K')
-        except RuntimeError:
-            pass
+    if graphs:
+        # The K launches' GPU time without the host's submission: the same
+        # graphs replayed once more right after the region, the stream kept
+        # busy by a ~100 us spin kernel while the host submits them, the
+        # events around the replays only (ROCm has no event nodes in graphs)
+        torch.cuda._sleep(200000)
+        g0e, g1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0e.record(stream)
+        for g in graphs:
+            g.replay()
+        g1e.record(stream)
+        torch.cuda.synchronize(dev)
+        gpu_ms_per_step = g0e.elapsed_time(g1e) / (args.steps - head)
+        gpu_timing = ('the timed region\'s %d graph-captured launches replayed once more right after it, back to back '
+                      'behind a spin kernel (so the host has submitted them): hipEvent pair / %d'
+                      % (args.steps - head, args.steps - head))
     dev_err = env.device_errors()
 
     # Kernel duration: launches timed one by one (hipEvent pair around each,

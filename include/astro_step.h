@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 13
+#define ASTRO_ABI_VERSION 14
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -229,6 +229,15 @@ int astro_stream_init(const AstroState *s, const uint32_t *stream_seeds, void *s
  * padding).  rows = p_pad + b_cap always suffices; objects past `rows` are
  * left out. */
 int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_t rows, void *stream);
+
+/* Host memory the kernels can address directly (the single-game path,
+ * astro_amd.core: a tick's state lives here, so a step is one launch and one
+ * synchronisation, no copies): `bytes` of page-locked, coherent host memory
+ * mapped into the device's address space.  *host is the CPU address,
+ * *device the address to put in AstroState / pass to the entry points.
+ * Every kernel access crosses PCIe: for one or a few games only. */
+int astro_host_alloc(uint64_t bytes, void **host, void **device);
+int astro_host_free(void *host);
 
 #ifdef __cplusplus
 }

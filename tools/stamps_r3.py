@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-section cycles of one step-wave launch from the -DASTRO_STAMPS build
+(tools/build_var.sh stamps ... -DASTRO_STAMPS): s_memtime stamps at section
+boundaries, one row per step wave (stats buffer), averaged over launches
+after a burn-in.  Round 3 adds stamps inside the bullet pass (16: bodies in
+LDS, 17: first rounds done) and after bullets_begin (19).
+    python tools/stamps_r3.py --workload c3 [--lib libastro_hip_stamps]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from astro_amd import BatchedEnv, DEFAULT_CONFIG, _lib  # noqa: E402
+
+NSTAMP = 24
+SEGS = dict(hdr_wait=(0, 1), bullets_begin=(1, 19), sincos_gravity=(19, 2), ship_collide=(2, 3),
+            bodies_lds=(3, 16), rounds_first=(16, 17), rounds_rest=(17, 4), reward_post=(4, 5),
+            spawn_ships=(5, 6), planets=(6, 7), hdr_store=(7, 8))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--workload', default='c3')
+    ap.add_argument('--lib', default='libastro_hip_stamps')
+    ap.add_argument('--ticks', type=int, default=20)
+    ap.add_argument('--warm', type=int, default=300)
+    a = ap.parse_args()
+    _lib._lib = None
+    _lib.load(os.path.join(ROOT, 'astro_amd', a.lib + '.so'))
+    w = bench.WORKLOADS[a.workload]
+    n = w['n']
+    env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=w['b_cap'], p_pad=w['p_pad'],
+                     auto_reset=True, planets_only=w['planets_only'])
+    env.reset()
+    lpe = dict(lane=1, quad=4, pair=2)[env.step_kernel]
+    nw = (n * lpe + 63) // 64
+    env.stats = torch.zeros(nw, NSTAMP, dtype=torch.int64, device='cuda')
+    env.rollout(a.warm, 'random', tick0=1 << 40, stats=False)
+    ctl = torch.from_numpy(bench.controls(0, n, env.S, a.ticks + 5)).cuda()
+    for t in range(5):
+        env.launch(ctl[t].data_ptr(), stats=False)
+    rows = []
+    for t in range(a.ticks):
+        env.stats.zero_()
+        env.launch(ctl[5 + t].data_ptr(), stats=True)
+        torch.cuda.synchronize()
+        rows.append(env.stats.cpu().numpy().astype(np.int64))
+    S = np.concatenate(rows, 0)
+    tot = S[:, 11] - S[:, 0]
+    out = dict(workload=a.workload, n=n, kernel=env.step_kernel, waves=nw, wave_cycles_mean=float(tot.mean()))
+    for k, (x, y) in SEGS.items():
+        ok = (S[:, x] > 0) & (S[:, y] > 0)
+        out[k] = [round(float((S[ok, y] - S[ok, x]).mean()), 1), round(float(ok.mean()), 3)] if ok.any() else None
+    rt = (S[:, 13] - S[:, 12]).astype(np.float64)
+    out['sclk_mhz'] = float((tot / np.maximum(rt, 1)).mean() * 100.0)
+    st, en = [], []
+    for t in range(a.ticks):
+        R = S[t * nw:(t + 1) * nw]
+        t0 = R[:, 12].min()
+        st.append((R[:, 12] - t0) / 100.0)
+        en.append((R[:, 13] - t0) / 100.0)
+    out['wave_start_us_mean'] = float(np.concatenate(st).mean())
+    out['wave_end_us_mean'] = float(np.concatenate(en).mean())
+    out['launch_last_wave_end_us'] = float(np.mean([e.max() for e in en]))
+    if (S[:, 21] > 0).any():
+        he = []
+        for t in range(a.ticks):
+            R = S[t * nw:(t + 1) * nw]
+            t0 = R[:, 12].min()
+            ok = R[:, 21] > 0
+            he.append(((R[ok, 21] - t0) / 100.0).max() if ok.any() else 0.0)
+        out['helper_last_end_us'] = float(np.mean(he))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()
