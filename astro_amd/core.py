@@ -9,12 +9,12 @@ the reference bit for bit (tests/test_gpu_parity.py): inputs are never
 mutated, a finished game returns ``(None, reward)`` with an int64 reward for
 a collision and a float32 reward for a timeout.
 
-This path is latency-bound by design: the game's arrays live in host memory
-the kernel addresses directly (``_MappedArena``, C-ABI astro_host_alloc), so
-a tick is one tiny launch and one synchronisation, no copies (``_Shim``);
+This path is latency-bound by design: a tick is one H2D copy of the packed
+state, one tiny launch, one D2H copy and a busy-polled event (``_Shim``);
 bulk simulation belongs on :class:`astro_amd.env.BatchedEnv`.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -31,14 +31,16 @@ def _device():
     return torch.device('cuda', torch.cuda.current_device())
 
 
-class _MappedArena:
-    """The arrays of one game packed (16-byte aligned) into page-locked host
-    memory that the kernels address directly (astro_host_alloc): numpy
-    views for the host, device addresses for AstroState.  No copies: a
-    kernel's loads and stores cross PCIe."""
+class _Arena:
+    """The arrays of one game packed (16-byte aligned) into one buffer, with
+    numpy views for the host and device addresses for AstroState.  mode
+    'copy': a device buffer mirrored by a pinned host buffer (one H2D copy
+    of a tick's input, one D2H copy back); mode 'mapped': page-locked host
+    memory the kernels address directly (astro_host_alloc; no copies, every
+    kernel access crosses PCIe)."""
 
-    def __init__(self, lib, specs):
-        self.lib = lib
+    def __init__(self, lib, specs, device, mode):
+        self.lib, self.mode = lib, mode
         self.layout = {}
         off = 0
         for name, shape, dt in specs:
@@ -46,15 +48,36 @@ class _MappedArena:
             self.layout[name] = (off, shape, dt, nbytes)
             off = (off + nbytes + 15) // 16 * 16
         self.nbytes = off
-        h, d = ctypes.c_void_p(), ctypes.c_void_p()
-        _lib.check(lib.astro_host_alloc(off, ctypes.byref(h), ctypes.byref(d)), 'astro_host_alloc')
-        self.host, self.device = h.value, d.value
-        raw = np.frombuffer((ctypes.c_uint8 * off).from_address(self.host), dtype=np.uint8)
+        self.host = None
+        if mode == 'mapped':
+            h, d = ctypes.c_void_p(), ctypes.c_void_p()
+            _lib.check(lib.astro_host_alloc(off, ctypes.byref(h), ctypes.byref(d)), 'astro_host_alloc')
+            self.host, self.device = h.value, d.value
+            raw = np.frombuffer((ctypes.c_uint8 * off).from_address(self.host), dtype=np.uint8)
+        else:
+            self.dev = torch.zeros(off, dtype=torch.uint8, device=device)
+            self.pinned = torch.zeros(off, dtype=torch.uint8).pin_memory()
+            self.device = self.dev.data_ptr()
+            raw = self.pinned.numpy()
         raw[:] = 0
         self.views = {n: raw[o:o + nb].view(dt).reshape(shape) for n, (o, shape, dt, nb) in self.layout.items()}
 
     def ptr(self, name):
         return self.device + self.layout[name][0]
+
+    def end(self, name):
+        o, _, _, nb = self.layout[name]
+        return o + nb
+
+    def push(self, upto):
+        """copy mode: host bytes [0, upto) to the device (stream-ordered)."""
+        if self.mode == 'copy':
+            self.dev[:upto].copy_(self.pinned[:upto], non_blocking=True)
+
+    def pull(self):
+        """copy mode: every byte back to the host (stream-ordered)."""
+        if self.mode == 'copy':
+            self.pinned.copy_(self.dev, non_blocking=True)
 
     def __del__(self):
         if getattr(self, 'host', None):
@@ -62,28 +85,37 @@ class _MappedArena:
             self.host = None
 
 
-class _Shim:
-    """One float64 game on the device for the single-game surface.  Its
-    state lives in host memory the kernel addresses directly (_MappedArena):
-    a tick writes the input into it, launches, synchronises and reads the
-    result -- one launch and one synchronisation, no copies."""
+# ASTRO_SHIM=mapped: the game's arrays in host memory the kernel addresses
+# directly; default 'copy' (measured faster on MI355X: a kernel's dependent
+# loads over PCIe cost more than two small copies, profiles/round3/)
+SHIM_MODE = os.environ.get('ASTRO_SHIM', 'copy')
 
-    def __init__(self, config, b_cap, device):
+
+class _Shim:
+    """One float64 game on the device for the single-game surface: its
+    arrays packed in one buffer (_Arena), a tick = the input written into
+    the host view, one H2D copy, one launch, one D2H copy, one wait for an
+    event (busy-polled: a blocking synchronisation wakes ~10-30 us late)."""
+
+    def __init__(self, config, b_cap, device, mode=None):
         self.env = env = BatchedEnv(config, 1, device=device, b_cap=b_cap, dtype=torch.float64,
                                     auto_reset=False, use_key_table=False)
         S, P = env.S, env.p_pad
         f8, i4 = np.float64, np.int32
-        self.arena = a = _MappedArena(env.lib, (
+        self.arena = a = _Arena(env.lib, (
             ('hdr', (1, 4), i4), ('ships', (S, 1, 4), f8), ('ships_b', (S, 1), f8), ('planets', (P, 1, 4), f8),
-            ('bullets', (1, b_cap, 4), f8), ('control', (1, S), np.int8), ('fire', (2,), i4),
-            ('reward', (1, S), np.float32), ('done', (1,), np.uint8), ('seed', (1,), np.uint32)))
+            ('bullets', (1, b_cap, 4), f8), ('control', (1, S), np.int8), ('fire', (2,), i4), ('seed', (1,), np.uint32),
+            ('reward', (1, S), np.float32), ('done', (1,), np.uint8), ('errors', (1,), np.uint32)),
+            env.device, mode or SHIM_MODE)
+        self.in_bytes = a.end('seed')   # hdr .. seed: a tick's input
+        self.event = torch.cuda.Event()
         self.h = a.views
-        # the env's own state record with its arrays moved to the mapped memory
-        # (its seed stream, error word and schedule stay the BatchedEnv's)
+        # the env's own state record with its arrays moved to the arena (its
+        # seed stream and schedule stay the BatchedEnv's)
         st = env.state
         self.state = type(st)(ships=a.ptr('ships'), ships_b=a.ptr('ships_b'), planets=a.ptr('planets'),
                               bullets=a.ptr('bullets'), hdr=a.ptr('hdr'), stream=st.stream,
-                              stream_ring=st.stream_ring, n_env=1, state_f64=1, errors=st.errors)
+                              stream_ring=st.stream_ring, n_env=1, state_f64=1, errors=a.ptr('errors'))
         # the launch's schedule per (first tick of a game?, times out?):
         # fire word = arena 'fire', timeout tick so `timeout` holds this call
         self.params = {}
@@ -98,11 +130,22 @@ class _Shim:
         return ctypes.c_void_p(torch.cuda.current_stream(self.env.device).cuda_stream)
 
     def sync(self):
-        torch.cuda.current_stream(self.env.device).synchronize()
-        self.env.check_errors()
+        """Results back to the host view; wait for them (busy-poll)."""
+        self.arena.pull()
+        ev = self.event
+        ev.record(torch.cuda.current_stream(self.env.device))
+        while not ev.query():
+            pass
+        bits = int(self.h['errors'][0])
+        if bits:
+            self.h['errors'][0] = 0
+            self.arena.push(self.arena.end('errors'))
+            why = '; '.join(m for b, m in sorted(_lib.ERRORS.items()) if bits & b) or 'unknown'
+            raise _lib.AstroError('astro_step reported device error 0x%x: %s' % (bits, why))
 
     def create(self, seed):
         self.h['seed'][0] = seed
+        self.arena.push(self.in_bytes)
         _lib.check(self.env.lib.astro_reset(ctypes.byref(self.env.params), ctypes.byref(self.state),
                                             self.arena.ptr('seed'), None, self.stream()), 'astro_reset')
         self.sync()
@@ -176,6 +219,7 @@ def step(state, control, config):
     h['control'][0] = control
     h['fire'][0] = int(fire) << tick
     a = sh.arena
+    a.push(sh.in_bytes)
     rc = env.lib.astro_step(ctypes.byref(sh.params[tick, bool(timeout)]), ctypes.byref(sh.state), a.ptr('control'),
                             a.ptr('reward'), a.ptr('done'), None, 0, sh.stream())
     if rc != 0:

@@ -123,8 +123,21 @@ def single_game_latency(cfg, ticks=2000, seed=0):
     """The single-game drop-in (astro_amd.core, what astro/server.py's
     game_tick and core.play's loop call): us per core.step tick with random
     controls, re-creating on termination, and us per tick of core.play with
-    two random bots (Bots.control + step + Tick bookkeeping)."""
+    two random bots (Bots.control + step + Tick bookkeeping); the shim's
+    default ('copy') and its host-mapped variant."""
     from astro_amd import core
+    out = {}
+    for mode in ('mapped', 'copy'):   # (the default last: its numbers are the line's)
+        core._ENVS.clear()
+        core.SHIM_MODE = mode
+        out.update(_single_game(core, cfg, ticks, seed))
+        out['us_per_step_' + mode] = out['us_per_step']
+    core.SHIM_MODE = os.environ.get('ASTRO_SHIM', 'copy')
+    core._ENVS.clear()
+    return out
+
+
+def _single_game(core, cfg, ticks, seed):
     rng = np.random.RandomState(seed)
     state = core.create(cfg)
     for _ in range(50):   # first calls: the shim's buffers, the kernels' first launch
@@ -150,8 +163,9 @@ def single_game_latency(cfg, ticks=2000, seed=0):
     dp = time.perf_counter() - t1
     return dict(us_per_step=dt / ticks * 1e6, steps=ticks, creates=n_create, us_per_play_tick=dp / played * 1e6,
                 play_ticks=played, games=k,
-                path='astro_amd.core.step: one H2D copy of the packed state, one launch, one D2H copy, '
-                     'one synchronisation per tick (float64 state, bit-exact to the reference)')
+                path='astro_amd.core.step (float64 state, bit-exact to the reference): per tick one H2D copy of '
+                     'the packed state, one launch, one D2H copy, one busy-polled event; "mapped": the state in '
+                     'host memory the kernel addresses directly, no copies')
 
 
 def _free_port():
@@ -251,7 +265,7 @@ def main():
                     help='secondary line: the workload as K-tick rollouts with the on-device random '
                          'policy, K ticks per launch (0 = skip)')
     ap.add_argument('--no-features', action='store_true', help='skip the observation-builder line')
-    ap.add_argument('--eager-head', type=int, default=4,
+    ap.add_argument('--eager-head', type=int, default=0,
                     help='timed launches issued eagerly before the graph replays: the GPU runs them while the '
                          'host submits the first graph (~10-40 us), so it does not idle at the start of the region')
     ap.add_argument('--no-single', action='store_true', help='skip the single-game drop-in latency line')
