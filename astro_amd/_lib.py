@@ -129,7 +129,10 @@ def load(path=LIB_PATH):
     # torch first: the library binds to the HIP runtime already in the process
     import torch  # noqa: F401
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    ab_any = os.environ.get('ASTRO_AB_ANY_ABI') == '1'
     for name, (res, args) in _SYMBOLS.items():
+        if ab_any and not hasattr(lib, name):   # (an older A/B build: entry points it predates)
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -231,18 +231,19 @@ def step(state, control, config):
         return None, reward.astype(np.int64)
     if done == 2:
         return None, reward.astype(np.float32)
-    nxt = sh.state_of()
+    # the next state straight from the returned arrays (float64 after a step;
+    # a lone planet's arrays stay float32; tick-0 bullets are float32)
     reload = state.reload + config.dt
     if fire:
         reload -= config.reload_time
     bdt = np.float32 if fresh else np.float64
+    pdt = np.float32 if npl == 1 else np.float64
+    nb2 = int(hdr[0, 1]) >> 16
+    sv, pl, bl = h['ships'][:, 0], h['planets'][:npl, 0], h['bullets'][0, :nb2]
     new = State(
-        ships=Bodies(x=nxt.ships.x.astype(np.float64), dx=nxt.ships.dx.astype(np.float64),
-                     b=nxt.ships.b.astype(np.float64)),
-        planets=Bodies(x=h['planets'][:npl, 0, 0:2].astype(np.float32 if npl == 1 else np.float64),
-                       dx=h['planets'][:npl, 0, 2:4].astype(np.float32 if npl == 1 else np.float64),
-                       b=None),
-        bullets=Bodies(x=nxt.bullets.x.astype(bdt), dx=nxt.bullets.dx.astype(bdt), b=None),
+        ships=Bodies(x=sv[:, 0:2].copy(), dx=sv[:, 2:4].copy(), b=h['ships_b'][:, 0].copy()),
+        planets=Bodies(x=pl[:, 0:2].astype(pdt), dx=pl[:, 2:4].astype(pdt), b=None),
+        bullets=Bodies(x=bl[:, 0:2].astype(bdt), dx=bl[:, 2:4].astype(bdt), b=None),
         reload=reload, t=state.t + config.dt)
     return new, np.zeros(S, dtype=np.float32)
 

@@ -1392,6 +1392,17 @@ __device__ __forceinline__ void bcast_slots(const T (&mine)[PPL], double (&out)[
     }
 }
 
+// a double from lane A/B/C/D of the caller's quad (DPP quad_perm(A,B,C,D):
+// lane i of the quad reads lane (A,B,C,D)[i])
+template <int A, int B, int C, int D>
+__device__ __forceinline__ double quad_perm_d(double v) {
+    constexpr int sel = A | (B << 2) | (C << 4) | (D << 6);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp(int(b & 0xffffffffll), sel, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), sel, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(uint32_t(lo)) | ((long long)hi << 32));
+}
+
 // a double from the other lane of the caller's pair (quad_perm(1,0,3,2))
 __device__ __forceinline__ double pair_swap(double v) {
     const long long b = __double_as_longlong(v);
@@ -1672,9 +1683,14 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     STAMP(18);
     if (on && fast) {
         if (u == 0) {   // the stream record and header, as restart_env
+#ifdef ASTRO_ABLATE_RESET_DRAW   // timing ablation only (wrong results): no stream draw, no stream memory
+            const uint32_t next_seed = mt_temper(seed * 2654435761u) & SEED_MASK;
+            (void)c;
+#else
             MTStream g{c.x, c.y, c.z, stream_ring_of(st, ie)};
             const uint32_t next_seed = g.next() & SEED_MASK;
             reinterpret_cast<uint4 *>(st.stream)[ie] = make_uint4(g.a, g.b, g.k, seed);
+#endif
             reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | (cf ? 2 << 8 : 0), int(next_seed), 0);
         }
     }
@@ -1752,6 +1768,24 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
         Fr[1][1] = l0 ? A2 : C;
         Fr[1][2] = l0 ? z : B;
         Fr[1][3] = l0 ? B2 : z;
+    }
+    // Quad kernel, 4 slots (config 2): lane q's planet is q; F(q, q + 1) and
+    // F(q, q + 2) (mod 4) computed here from the neighbours' planets (DPP
+    // rotations), F(q, q + 3) = F(q + 3, q) is lane q + 3's first: 2 divisions
+    // per lane instead of field()'s 4 (self term included)
+    if constexpr (LPE == 4 && PMAX == 4) {
+        const double ox = double(mpx[0]), oy = double(mpy[0]);
+        const double x1 = quad_perm_d<1, 2, 3, 0>(ox), y1 = quad_perm_d<1, 2, 3, 0>(oy);
+        const double x2 = quad_perm_d<2, 3, 0, 1>(ox), y2 = quad_perm_d<2, 3, 0, 1>(oy);
+        const double dx1 = x1 - ox, dy1 = y1 - oy, dx2 = x2 - ox, dy2 = y2 - oy;
+        const double A = div_gravity(p.gm, max_floor(dx1 * dx1 + dy1 * dy1));   // F(q, q + 1)
+        const double B = div_gravity(p.gm, max_floor(dx2 * dx2 + dy2 * dy2));   // F(q, q + 2)
+        const double C = quad_perm_d<3, 0, 1, 2>(A);                              // F(q, q + 3)
+#pragma unroll
+        for (int k = 0; k < PMAX; ++k) {
+            const int d = (k - q) & 3;   // (self, d == 0: unused)
+            Fr[0][k] = d == 1 ? A : (d == 2 ? B : C);
+        }
     }
     // Pair kernel, 8 slots (config 5): the 28 distinct pair factors, 14 per
     // lane instead of 32 (each own planet's 8 terms), exchanged by DPP.
@@ -1831,7 +1865,7 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
                     gx = px[1] - pxj;
                     gy = py[1] - pyj;
 #else
-                    if constexpr (LPE == 2 && (PMAX == 4 || PMAX == 8)) {
+                    if constexpr ((LPE == 2 && (PMAX == 4 || PMAX == 8)) || (LPE == 4 && PMAX == 4)) {
                         // field<double> at planet j from the shared factors:
                         // term k = F(j, k) * (p_k - p_j) summed in k order; the
                         // self term is gm / 1e-12 * (+0), a zero with gm's sign
@@ -1970,12 +2004,17 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroState &st, size
     b.total = __builtin_amdgcn_readlane(incl, 63);
 #endif
     b.tag = bw_tag(e, np, t0);
-    index_window<LPE>(s_index, 0, b.off, nb, q, b.tag);
     if (q == 0) {
         s_kept[e] = 0;
         s_hit[e] = 0;
         s_serial[e] = 0;
     }
+    if (b.total == 0) {   // uniform: no live bullet in the wave (config 2): no index, no loads
+        b.bw0 = b.bw1 = 0u;
+        b.cur0 = b.cur1 = V{};
+        return b;
+    }
+    index_window<LPE>(s_index, 0, b.off, nb, q, b.tag);
     wave_sync();
     b.bw0 = lane < b.total ? s_index[lane] : 0u;
     b.bw1 = lane + 64 < min(b.total, QWIN) ? s_index[lane + 64] : 0u;
@@ -2006,6 +2045,10 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
     const uint32_t tag = b.tag;
     uint32_t bw0 = b.bw0, bw1 = b.bw1;
     V cur0 = b.cur0, cur1 = b.cur1;
+    if (total == 0) {   // uniform: nothing to do (bullets_begin left s_kept, s_hit cleared)
+        wave_sync();
+        return;
+    }
     // ---- old positions of the env's bodies for the bullet pass (LDS)
     {
         float2 *body = reinterpret_cast<float2 *>(&s_body[e][0]);
@@ -2361,7 +2404,11 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                     if (j < np) planets[size_t(j) * NN + i] = hout[m];
                 }
             }
+#ifdef ASTRO_ABLATE_RESETS   // timing ablation only (wrong results): the helpers create no game
+            if (false) {
+#else
             if (todo0) {   // uniform
+#endif
                 for (uint64_t todo = todo0; todo;)   // uniform
                     todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, s_chain,
                                                                   s_serial STAMP_PASS, pre);
@@ -2533,6 +2580,36 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     np_sincosf(float(mb), ds, dc);
 #endif
     double ax = 0.0, ay = 0.0;
+    // Quad kernel, 4 slots: the ships' float64 fields split over the quad --
+    // lane q evaluates ship (q & 1)'s terms of planet slots q >> 1 and
+    // (q >> 1) + 2, and the ship's lane adds them in slot order (2 divisions
+    // per lane instead of 3-4 on the ship lanes alone)
+    double sgx = 0.0, sgy = 0.0;
+    if constexpr (LPE == 4 && PMAX == 4) {
+        double s0x = sx[0], s0y = sy[0], s1x = sx[S - 1], s1y = sy[S - 1];
+        double p0x = px[0], p0y = py[0], p1x = px[1], p1y = py[1], p2x = px[2], p2y = py[2], p3x = px[3], p3y = py[3];
+        asm volatile("" : "+v"(s0x), "+v"(s0y), "+v"(s1x), "+v"(s1y));   // (selects, not an indexed array)
+        asm volatile("" : "+v"(p0x), "+v"(p0y), "+v"(p1x), "+v"(p1y), "+v"(p2x), "+v"(p2y), "+v"(p3x), "+v"(p3y));
+        const bool odd = (q & 1) != 0, hi = q >= 2;
+        const double shx = odd ? s1x : s0x, shy = odd ? s1y : s0y;
+        const double ax_ = hi ? p1x : p0x, ay_ = hi ? p1y : p0y;   // slot q >> 1
+        const double bx_ = hi ? p3x : p2x, by_ = hi ? p3y : p2y;   // slot (q >> 1) + 2
+        const double rax = ax_ - shx, ray = ay_ - shy, rbx = bx_ - shx, rby = by_ - shy;
+        const double fa = div_gravity(p.gm, max_floor(rax * rax + ray * ray));
+        const double fb = div_gravity(p.gm, max_floor(rbx * rbx + rby * rby));
+        const double tax = fa * rax, tay = fa * ray, tbx = fb * rbx, tby = fb * rby;
+        // the ship's lane (q < 2) holds slots 0 and 2; slots 1 and 3 from lane q + 2
+        const double t1x = quad_perm_d<2, 3, 2, 3>(tax), t1y = quad_perm_d<2, 3, 2, 3>(tay);
+        const double t3x = quad_perm_d<2, 3, 2, 3>(tbx), t3y = quad_perm_d<2, 3, 2, 3>(tby);
+        sgx = tax;
+        sgy = tay;
+        sgx = 1 < np ? sgx + t1x : sgx;
+        sgy = 1 < np ? sgy + t1y : sgy;
+        sgx = 2 < np ? sgx + tbx : sgx;
+        sgy = 2 < np ? sgy + tby : sgy;
+        sgx = slot_last && 3 < np ? sgx + t3x : sgx;
+        sgy = slot_last && 3 < np ? sgy + t3y : sgy;
+    }
     if (q < S) {
         double gx, gy;
         if (t0) {
@@ -2545,7 +2622,12 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             gx = px[0] - mx;
             gy = py[0] - my;
 #else
-            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
+            if constexpr (LPE == 4 && PMAX == 4) {
+                gx = sgx;
+                gy = sgy;
+            } else {
+                field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
+            }
 #endif
         }
         const double thr = p.thrust * double(ctl & 1);

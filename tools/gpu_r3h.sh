@@ -1,0 +1,23 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/r3h
+mkdir -p $O
+step() {
+  local name=$1 limit=$2; shift 2
+  timeout -k 10 "$limit" "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  grep -E "^\{|passed|failed|Error" $O/$name.log | tail -4 | cut -c1-1500
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  return $rc
+}
+step pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
+export ASTRO_AB_ANY_ABI=1
+step ab_c2 300 python tools/ab.py --libs libastro_hip_r2,libastro_hip_cur,libastro_hip_q4 --workload c2 --rounds 5
+step ab_c3 300 python tools/ab.py --libs libastro_hip_r2,libastro_hip_cur,libastro_hip_q4 --workload c3 --rounds 4
+step vs_c2 200 python tools/varstats.py --libs libastro_hip_cur,libastro_hip_q4 --workload c2
+step stamps_c3 200 python tools/stamps_r3.py --workload c3 --lib libastro_hip_stamps --ticks 40
+step stamps_c2 200 python tools/stamps_r3.py --workload c2 --lib libastro_hip_stamps --ticks 40
+exit 0

@@ -76,6 +76,24 @@ def main():
             ok = R[:, 21] > 0
             he.append(((R[ok, 21] - t0) / 100.0).max() if ok.any() else 0.0)
         out['helper_last_end_us'] = float(np.mean(he))
+    # what makes a wave slow: its live bullets, games at their first tick,
+    # finished games (stamp 15 = resets | t0 << 8 | bullets << 16)
+    info = S[:, 15]
+    nres, nt0, nbul = info & 0xff, (info >> 8) & 0xff, (info >> 16) & 0xffff
+    cyc = tot.astype(np.float64)
+    slow = cyc >= np.percentile(cyc, 95)
+    out['slow5'] = dict(cycles=float(cyc[slow].mean()), bullets=float(nbul[slow].mean()), t0=float(nt0[slow].mean()),
+                        resets=float(nres[slow].mean()), start_us=float(np.concatenate(st)[slow].mean()))
+    out['all'] = dict(cycles=float(cyc.mean()), bullets=float(nbul.mean()), t0=float(nt0.mean()), resets=float(nres.mean()))
+    A = np.stack([np.ones_like(cyc), nbul, nt0, nres], 1).astype(np.float64)
+    coef = np.linalg.lstsq(A, cyc, rcond=None)[0]
+    out['fit_cycles'] = dict(base=float(coef[0]), per_bullet=float(coef[1]), per_t0=float(coef[2]), per_reset=float(coef[3]))
+    for k in SEGS:
+        x, y = SEGS[k]
+        ok = (S[:, x] > 0) & (S[:, y] > 0)
+        if ok.any():
+            d = (S[:, y] - S[:, x]).astype(np.float64)
+            out.setdefault('slow5_seg', {})[k] = round(float(d[slow & ok].mean()), 1) if (slow & ok).any() else None
     print(json.dumps(out), flush=True)
 
 
