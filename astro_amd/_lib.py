@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # (ASTRO_LIB: another build of the same library, e.g. an A/B variant from tools/build_var.sh)
 LIB_PATH = os.environ.get('ASTRO_LIB') or os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')

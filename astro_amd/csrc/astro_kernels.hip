@@ -325,10 +325,16 @@ __device__ __forceinline__ uint32_t mt_key_at(uint32_t v, uint32_t from, uint32_
 
 constexpr uint32_t MT_PROLOGUE = 397;
 
-// hdr word 0 = tick | KEY_VALID (hdr word 3 holds key[397] of the pending seed)
+// hdr word 0 = tick; word 2 = pending seed | KEY_VALID (word 3 then holds
+// key[397] of the pending seed), or UNDRAWN: a reset leaves the next game's
+// seed in the stream, for the env's first step (or its helper) to draw off
+// the reset path.  The words a step rewrites for a surviving
+// env are split: 0-1 (tick, counts) by the step wave, 2-3 (pending seed and
+// key) by whoever checks the pending seed -- the step wave, or its helper
 constexpr int TICK_BITS = 22;
 constexpr uint32_t TICK_MASK = (1u << TICK_BITS) - 1;
 constexpr uint32_t KEY_VALID = 1u << 31;
+constexpr uint32_t UNDRAWN = 1u << 30;
 constexpr uint32_t SEED_MASK = (1u << 30) - 1;   // generate_configs seeds are randint(1 << 30)
 
 struct MTLazy {
@@ -657,8 +663,9 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, con
 
 // Start env i's next game: its seed was drawn one game ahead (hdr word 2) and
 // key[397] of that seed fetched from the key table by an earlier step (hdr
-// word 3, valid when KEY_VALID); create, then draw the following seed.  The
-// following seed's key is gathered by the NEXT step, off this path.
+// word 3, valid when KEY_VALID) -- unless the game ended at its first step
+// (UNDRAWN: draw it here); create.  The following seed is drawn, and its key
+// gathered, by the NEXT step, off this path.
 // Everything integer about an env's next game: the create() words of its
 // pending seed and the stream cursor advanced by one game (core.py:83).
 template <int S>
@@ -667,17 +674,17 @@ struct NextGame {
                            // planets_only the first of the stream to pass)
     CreateWords<S> words;
     uint32_t ca, cb, ci;   // advanced cursor
-    uint32_t next_seed;    // the game after
     bool exhausted;        // create() ran past the 227 words MTLazy covers
 };
 
 // (key397 of the pending seed is either known or, have_key false, run here)
 template <int S>
 __device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t pend_seed, uint32_t key397,
-                                                 bool have_key, const uint4 &c, uint32_t *ring) {
+                                                 bool have_key, bool undrawn, const uint4 &c, uint32_t *ring) {
     NextGame<S> ng;
     MTStream g{c.x, c.y, c.z, ring};
-    if (!have_key) key397 = mt_key_at(pend_seed, 0, MT_PROLOGUE);
+    if (undrawn) pend_seed = g.next() & SEED_MASK;
+    if (!have_key || undrawn) key397 = key397_of(p, pend_seed);
     // planets_only: the pending seed may not have been checked yet (a game
     // shorter than the steps that check one candidate each): walk the
     // stream here, synchronously
@@ -688,7 +695,6 @@ __device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t 
     ng.seed = pend_seed;
     ng.words = create_words<S>(p, pend_seed, key397);
     ng.exhausted = ng.words.exhausted;
-    ng.next_seed = g.next() & SEED_MASK;
     ng.ca = g.a;
     ng.cb = g.b;
     ng.ci = g.k;
@@ -705,21 +711,24 @@ __device__ __forceinline__ void restart_env(const AstroParams &p, const AstroSta
     if (part != 0) return;
     reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(ng.ca, ng.cb, ng.ci, ng.seed);
     const int flags = (ng.exhausted || cf) ? 2 : 0;
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(ng.next_seed), 0);
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(UNDRAWN), 0);
 }
 
 // The pending seed at the end of a step (the lane holding the env's header):
-// key[397] of a pending seed is gathered by the first step that finds it
-// missing (KEY_VALID); with planets_only, that step also checks the seed and,
-// if its game has the wrong number of planets, draws the stream's next one
-// instead (cursor c, loaded beside the gather) for the following step to
+// an UNDRAWN one is drawn (cursor c); key[397] of a pending seed is gathered
+// by the first step that finds it missing (KEY_VALID); with planets_only,
+// that step also checks the seed and, if its game has the wrong number of
+// planets, draws the stream's next one instead for the following step to
 // check -- one candidate per step, off the reset path.  Returns the
-// KEY_VALID bit for the header.
+// KEY_VALID bit for the header.  (The draws do not depend on the key table:
+// the stream cursor evolves identically with and without it.)
 __device__ __forceinline__ uint32_t check_pending(const AstroParams &p, const AstroState &st, int i, bool key_valid,
-                                                  const uint4 &c, uint32_t &seed, uint32_t &key) {
+                                                  bool undrawn, const uint4 &c, uint32_t &seed, uint32_t &key) {
     if (key_valid) return KEY_VALID;
-    if (!p.key_table) return 0u;
-    if (seed_passes(p, seed, key)) return KEY_VALID;
+    if (!undrawn) {
+        if (!p.key_table) return 0u;
+        if (seed_passes(p, seed, key)) return KEY_VALID;
+    }
     MTStream g{c.x, c.y, c.z, stream_ring_of(st, i)};
     seed = g.next() & SEED_MASK;
     key = 0u;
@@ -1077,8 +1086,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             for (int s = 0; s < S; ++s) ctl[s] = tick_control<S>(drv, i, s, NN, 0);
         }
         const int tick = int(uint32_t(h.x) & TICK_MASK);
-        const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
-        uint32_t pend_seed = uint32_t(h.z);
+        const bool key_valid = (uint32_t(h.z) & KEY_VALID) != 0;
+        const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
+        uint32_t pend_seed = uint32_t(h.z) & SEED_MASK;
         int np = h.y & 0xff;
         int flags = (h.y >> 8) & 0xff;
         const int nb = int(uint32_t(h.y) >> 16);
@@ -1103,9 +1113,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
         // key[397] of the next game's seed, fetched once per game, off the reset path
         uint32_t pend_key = uint32_t(h.w);
-        if (!key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
+        if (!key_valid && !undrawn && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
         // stream cursor, for check_pending: loaded branch-free, see the quad kernel
-        const bool want_c = !key_valid && p.key_table && p.planets_only;
+        const bool want_c = undrawn || (!key_valid && p.key_table && p.planets_only);
         uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
         asm volatile("" : "+v"(c_stream), "+v"(c_hdr));
         const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
@@ -1288,9 +1298,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             }
             STAMP(7);
             if (dropped) flags |= 1;
-            const uint32_t kv = check_pending(p, st, i, key_valid, c_pend, pend_seed, pend_key);
+            const uint32_t kv = check_pending(p, st, i, key_valid, undrawn, c_pend, pend_seed, pend_key);
             reinterpret_cast<int4 *>(st.hdr)[i] =
-                make_int4(int(uint32_t(tick + 1) | kv), np | (flags << 8) | (w << 16), int(pend_seed), int(pend_key));
+                make_int4(tick + 1, np | (flags << 8) | (w << 16), int(pend_seed | kv), int(pend_key));
             n_bout = uint32_t(w);
             n_drop = uint32_t(dropped);
             STAMP(8);
@@ -1300,7 +1310,8 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             f_tout = timeout;
             if (auto_reset) {
                 const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-                const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, c, stream_ring_of(st, i));
+                const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, undrawn, c,
+                                                    stream_ring_of(st, i));
                 restart_env<T, S, PMAX>(p, st, i, ng);
                 f_reset = true;
             }
@@ -1589,11 +1600,13 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
 // output instead of two chains plus tempering; the float work of create()
 // then runs spread over the row (ship u, planet u).  An env whose first
 // randint word is rejected is flagged in s_serial for the quad's serial
-// create.  Returns the leaders not yet served.
+// create, and so is one whose game ended at its first step (its seed still
+// UNDRAWN).  The stream cursor is left alone: the next game's seed is drawn
+// by the env's first step.  Returns the leaders not yet served.
 template <typename T, int S, int PMAX, int LPE, bool PRE = false>
 __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
                                                     int lane, int i, uint32_t pend_seed, uint32_t pend_key,
-                                                    bool have_key, uint32_t (*s_chain)[2][13 + 2 * S],
+                                                    bool have_key, bool undrawn, uint32_t (*s_chain)[2][13 + 2 * S],
                                                     int *s_serial STAMP_ARG,
                                                     const uint32_t (*pre)[2][13 + 2 * S] = nullptr) {
     constexpr int NW = 12 + 2 * S;   // outputs create() draws, randint accepting its first word
@@ -1611,7 +1624,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     const uint32_t seed = uint32_t(__shfl(int(pend_seed), src, 64));
     const uint32_t key = uint32_t(__shfl(int(pend_key), src, 64));
     const bool hk = __shfl(int(have_key), src, 64) != 0;
-    const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[ie];   // used last: in flight meanwhile
+    const bool ud = __shfl(int(undrawn), src, 64) != 0;
 
     const int uw = u < NW ? u : 0;
     uint32_t a0, a1, b0;
@@ -1652,7 +1665,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     mask |= mask >> 8;
     mask |= mask >> 16;
     const uint32_t v = uint32_t(__shfl(int(w), row0, 64)) & mask;
-    const bool fast = rng != 0 && v <= rng && (p.planets_only == 0 || int(v) + 1 == p.planets_only);
+    const bool fast = !ud && rng != 0 && v <= rng && (p.planets_only == 0 || int(v) + 1 == p.planets_only);
     // lane k of the row: R_k = rand() of outputs k, k + 1
     const uint32_t wn = uint32_t(__shfl(int(w), row0 | ((u + 1) & 15), 64));
     const double R = rand53(w, wn);
@@ -1682,16 +1695,9 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     }
     STAMP(18);
     if (on && fast) {
-        if (u == 0) {   // the stream record and header, as restart_env
-#ifdef ASTRO_ABLATE_RESET_DRAW   // timing ablation only (wrong results): no stream draw, no stream memory
-            const uint32_t next_seed = mt_temper(seed * 2654435761u) & SEED_MASK;
-            (void)c;
-#else
-            MTStream g{c.x, c.y, c.z, stream_ring_of(st, ie)};
-            const uint32_t next_seed = g.next() & SEED_MASK;
-            reinterpret_cast<uint4 *>(st.stream)[ie] = make_uint4(g.a, g.b, g.k, seed);
-#endif
-            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | (cf ? 2 << 8 : 0), int(next_seed), 0);
+        if (u == 0) {   // the stream record's game seed and the header, as restart_env
+            st.stream[4 * size_t(ie) + 3] = seed;
+            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | (cf ? 2 << 8 : 0), int(UNDRAWN), 0);
         }
     }
     if (on && !fast && u == 0) s_serial[L / LPE] = 1;
@@ -1903,6 +1909,15 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
     }
 
 }
+
+// The helper waves check their step waves' pending seeds (check_pending's
+// draw, key gather, filter and redraw) and store header words 2-3 of the
+// survivors; the step waves only write words 0-1.  1: quad instance only
+// (its step waves are the critical path: c2 5.36 -> 5.20 us A/B), 2: pair
+// too (there the helpers' resets are the tail: c3 12.19 -> 12.52 us), 0: off
+#ifndef ASTRO_PENDING_ON_HELPER
+#define ASTRO_PENDING_ON_HELPER 1
+#endif
 
 // The step wave waits for its helper's header read (HelpBox.seen) before it
 // rewrites the headers (A/B knob)
@@ -2266,6 +2281,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     __shared__ uint32_t s_pre_all[HELP ? WPG : 1][HELP ? QENV : 1][2][13 + 2 * S];   // a helper's chains, made ahead
     // (wave_sync syncs one wave whenever the build's QW > 1, whatever this instance's WPG)
     static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, wave-scoped LDS sync");
+    constexpr bool PENDING_ON_HELPER = HELP && (ASTRO_PENDING_ON_HELPER == 2 || (ASTRO_PENDING_ON_HELPER == 1 && LPE == 4));
     const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
     const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
     float4 (*s_body)[NBOD2] = s_body_all[wv];
@@ -2312,11 +2328,43 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             // launch's input whatever the memory system's timing (the store
             // depends on the loaded value: it waits for the load's return)
             if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
-            const uint32_t hseed = uint32_t(hh.z);
-            const bool kvalid = (uint32_t(hh.x) & KEY_VALID) != 0;
+            const uint32_t hseed = uint32_t(hh.z) & SEED_MASK;
+            const bool kvalid = (uint32_t(hh.z) & KEY_VALID) != 0;
+            const bool hud = (uint32_t(hh.z) & UNDRAWN) != 0;   // (a reset then takes the serial path)
             uint32_t hkey = uint32_t(hh.w);
             const bool hk = kvalid || p.key_table != nullptr;
-            if (q == 1 && !kvalid) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
+            if (q == 1 && !kvalid && !hud) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
+            // ... and (PENDING_ON_HELPER) the step wave's check of every env's
+            // pending seed, as check_pending does it: the draw of a first-step
+            // env's UNDRAWN seed, key[397] of a pending seed, and with
+            // planets_only the seed's planet count (a failing seed is
+            // replaced by the stream's next draw).  The
+            // results -- header words 2-3 and the advanced stream cursor -- are
+            // stored for the surviving envs after the post (a finished env's
+            // reset starts from the unchecked pending seed and the cursor in
+            // memory, as without helpers)
+            uint32_t w2 = uint32_t(hh.z), w3 = uint32_t(hh.w);   // the survivors' header words 2-3
+            bool drew = false;
+            uint4 cnew = make_uint4(0u, 0u, 0u, 0u);
+            if constexpr (PENDING_ON_HELPER) {
+                if (q == 0 && active && (hud || (!kvalid && p.key_table))) {   // (rare: a game's first steps)
+                    bool draw = hud;
+                    if (!hud) {
+                        const uint32_t k397 = p.key_table[hseed];
+                        w3 = k397;
+                        if (seed_passes(p, hseed, k397)) w2 = hseed | KEY_VALID;
+                        else draw = true;   // (planets_only) the next candidate, checked next launch
+                    }
+                    if (draw) {
+                        const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+                        MTStream g{c.x, c.y, c.z, stream_ring_of(st, i)};   // (its ring store is the same
+                        w2 = g.next() & SEED_MASK;                           //  word whoever draws it)
+                        w3 = 0u;
+                        cnew = make_uint4(g.a, g.b, g.k, c.w);
+                        drew = true;
+                    }
+                }
+            }
             // ... and, pair instance, the planet update of every env of the
             // step wave (the survivors' stored after the post; the step wave
             // then skips it: c3 12.39 -> 11.92 us with eight step waves per
@@ -2404,20 +2452,24 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                     if (j < np) planets[size_t(j) * NN + i] = hout[m];
                 }
             }
+            if (PENDING_ON_HELPER && q == 0 && active && !((todo0 >> lane) & 1ull)) {   // a surviving env: its
+                reinterpret_cast<int2 *>(st.hdr)[2 * i + 1] = make_int2(int(w2), int(w3));   // pending seed
+                if (drew) reinterpret_cast<uint4 *>(st.stream)[i] = cnew;
+            }
 #ifdef ASTRO_ABLATE_RESETS   // timing ablation only (wrong results): the helpers create no game
             if (false) {
 #else
             if (todo0) {   // uniform
 #endif
                 for (uint64_t todo = todo0; todo;)   // uniform
-                    todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, s_chain,
+                    todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, hud, s_chain,
                                                                   s_serial STAMP_PASS, pre);
                 wave_sync();
                 if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
                 if (active && s_serial[e]) {   // uniform over the quad; rare
                     const uint32_t kq = uint32_t(quad_bcast_i<1, LPE>(int(hkey)));   // (lane q == 1 has the key)
                     const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-                    const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, c, stream_ring_of(st, i));
+                    const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, hud, c, stream_ring_of(st, i));
                     restart_env<T, S, PMAX, LPE>(p, st, i, ng, q);
                 }
             }
@@ -2479,8 +2531,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         }
     }
     const int tick = int(uint32_t(h.x) & TICK_MASK);
-    const bool key_valid = (uint32_t(h.x) & KEY_VALID) != 0;
-    uint32_t pend_seed = uint32_t(h.z);
+    const bool key_valid = (uint32_t(h.z) & KEY_VALID) != 0;
+    const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
+    uint32_t pend_seed = uint32_t(h.z) & SEED_MASK;
     int np = h.y & 0xff;
     const int flags = (h.y >> 8) & 0xff;
     const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
@@ -2527,14 +2580,21 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // key[397] of the next game's seed (first step of a game): a random
     // gather into the 4 GiB key table, issued after every load the physics
     // waits for, so only its consumers (header store, reset) wait for it
-    if (q == 0 && !key_valid && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
+#ifndef ASTRO_ABLATE_PENDING
+    if (!PENDING_ON_HELPER && q == 0 && !key_valid && !undrawn && p.key_table)
+        pend_key = p.key_table[pend_seed & SEED_MASK];
+#endif
     // stream cursor, for check_pending (read there under this same condition
     // only).  Every lane loads, the others their own header again (the line
     // just read: no traffic).  A conditional load made the compiler merge
     // its value with the other lanes' zeros right after it, i.e. wait for it
     // -- and for every load before it, the key-table gather included -- at
     // the top of the wave (c3 13.10 -> 12.65 us, c2 6.74 -> 6.64 us, A/B)
-    const bool want_c = q == 0 && !key_valid && p.key_table && p.planets_only;
+#ifdef ASTRO_ABLATE_PENDING   // timing ablation only (wrong results): the step wave does no pending-seed work
+    const bool want_c = false;
+#else
+    const bool want_c = !PENDING_ON_HELPER && q == 0 && (undrawn || (!key_valid && p.key_table && p.planets_only));
+#endif
     uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
     asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // values, not a select between the fields' addresses
     const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
@@ -2800,9 +2860,17 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             STAMP(7);
             if (q == 0) {
                 const int fl = flags | (dropped ? 1 : 0);
-                const uint32_t kv = check_pending(p, st, is, key_valid, c_pend, pend_seed, pend_key);
-                reinterpret_cast<int4 *>(st.hdr)[is] =
-                    make_int4(int(uint32_t(tick + 1) | kv), np | (fl << 8) | (w << 16), int(pend_seed), int(pend_key));
+                if constexpr (PENDING_ON_HELPER) {   // words 2-3: the helper's
+                    reinterpret_cast<int2 *>(st.hdr)[2 * is] = make_int2(tick + 1, np | (fl << 8) | (w << 16));
+                } else {
+#ifdef ASTRO_ABLATE_PENDING
+                    const uint32_t kv = key_valid ? KEY_VALID : 0u;
+#else
+                    const uint32_t kv = check_pending(p, st, is, key_valid, undrawn, c_pend, pend_seed, pend_key);
+#endif
+                    reinterpret_cast<int4 *>(st.hdr)[is] =
+                        make_int4(tick + 1, np | (fl << 8) | (w << 16), int(pend_seed | kv), int(pend_key));
+                }
                 n_bout += uint32_t(w);
                 n_drop += uint32_t(dropped);
             }
@@ -2822,14 +2890,15 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     if constexpr (!HELP)
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
         todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
-                                           s_chain, s_serial STAMP_PASS);
+                                           undrawn, s_chain, s_serial STAMP_PASS);
     if (!HELP && auto_reset) {
         wave_sync();
         if (stats) c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));
         if (active && s_serial[e]) {   // uniform over the quad; rare
             const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(pend_key)));   // lane q == 0 fetched it
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
-            const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, c, stream_ring_of(st, is));
+            const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, undrawn, c,
+                                                stream_ring_of(st, is));
             restart_env<T, S, PMAX, LPE>(p, st, is, ng, q);
         }
     }
@@ -3058,10 +3127,11 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
     if (mask && !mask[i]) return;
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
     if (!seeds) {
-        const uint32_t seed = uint32_t(h.z);
-        const uint32_t key = (uint32_t(h.x) & KEY_VALID) ? uint32_t(h.w) : key397_of(p, seed);
+        const uint32_t seed = uint32_t(h.z) & SEED_MASK;
+        const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
+        const uint32_t key = (uint32_t(h.z) & KEY_VALID) ? uint32_t(h.w) : undrawn ? 0u : key397_of(p, seed);
         const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, c, stream_ring_of(st, i)));
+        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, undrawn, c, stream_ring_of(st, i)));
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued

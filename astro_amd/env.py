@@ -16,8 +16,9 @@ per env (the kernels walk an env's live bullets in slot order):
 
     ships    [S, N, 4]   x, y, dx, dy        ships_b  [S, N]
     planets  [P, N, 4]   x, y, dx, dy        bullets  [N, B, 4]
-    hdr      [N, 4]      tick | chain << 22, nplanets | flags << 8 | nbullets << 16,
-                         next game's init-chain value, next game's seed
+    hdr      [N, 4]      tick, nplanets | flags << 8 | nbullets << 16,
+                         next game's seed | key_valid << 31 (or undrawn << 30: the
+                         game's first step draws it), key[397] of its init chain
     stream   [N, 4]      seed-stream cursor + current game's seed
     stream_ring [N, 624] the stream's MT19937 state words (exact for any length)
 

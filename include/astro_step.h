@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 14
+#define ASTRO_ABI_VERSION 15
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -90,9 +90,11 @@ enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2, ASTR
 #define ASTRO_QUAD_MAX_ENVS 32768
 
 /* Per-env state arrays (device pointers).  hdr packs
- *   hdr[4*i+0] = tick (steps since create, < 2^22) | key_valid << 31
+ *   hdr[4*i+0] = tick (steps since create, < 2^22)
  *   hdr[4*i+1] = nplanets | flags << 8 | nbullets << 16
- *   hdr[4*i+2] = the NEXT game's seed (drawn one game ahead from the stream)
+ *   hdr[4*i+2] = the NEXT game's seed (drawn one game ahead from the stream,
+ *                < 2^30) | key_valid << 31, or undrawn << 30 alone: a game's
+ *                create leaves the draw to its first step, off the reset path
  *   hdr[4*i+3] = key[397] of that seed's MT19937 init chain (when key_valid)
  * flags: bit0 = a bullet was dropped (b_cap full) this game,
  *        bit1 = create() needed more than 227 words of its seed's MT19937
