@@ -76,6 +76,30 @@ def main():
             ok = R[:, 21] > 0
             he.append(((R[ok, 21] - t0) / 100.0).max() if ok.any() else 0.0)
         out['helper_last_end_us'] = float(np.mean(he))
+        # the helpers after the post: stamp 20 = post seen, 21 = end (both
+        # s_memrealtime), 22 = finished envs posted
+        ok = (S[:, 20] > 0) & (S[:, 21] > 0)
+        nr = S[:, 22]
+        aft = (S[:, 21] - S[:, 20]) / 100.0
+        out['helper_after_post_us'] = {str(k): [round(float(aft[ok & (np.minimum(nr, 2) == k)].mean()), 3),
+                                               int((ok & (np.minimum(nr, 2) == k)).sum())]
+                                       for k in (0, 1, 2) if (ok & (np.minimum(nr, 2) == k)).any()}
+        post = []
+        for t in range(a.ticks):
+            R = S[t * nw:(t + 1) * nw]
+            t0 = R[:, 12].min()
+            okr = R[:, 20] > 0
+            post.append(((R[okr, 20] - t0) / 100.0).mean() if okr.any() else 0.0)
+        out['helper_post_seen_us_mean'] = float(np.mean(post))
+        # of the launch's 1% last-ending helpers: how many had resets
+        ends = []
+        for t in range(a.ticks):
+            R = S[t * nw:(t + 1) * nw]
+            okr = R[:, 21] > 0
+            e = R[okr, 21]
+            cut = np.percentile(e, 99)
+            ends.append(float((R[okr][e >= cut, 22] > 0).mean()))
+        out['helper_top1pct_with_resets'] = float(np.mean(ends))
     # what makes a wave slow: its live bullets, games at their first tick,
     # finished games (stamp 15 = resets | t0 << 8 | bullets << 16)
     info = S[:, 15]
