@@ -1518,6 +1518,53 @@ __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off,
     if (k1 == nb && k1 > k0) dst[-1] = w - (1u << 5) + (1u << 21);   // last of the env
 }
 
+// create()'s ship s (second: s == 1 of two) and planet values from the
+// draws and the direction()s (core.py:93-121); shared by the reset pass and
+// the pair helpers' pre-create so that both are the same arithmetic
+template <typename T, int S>
+__device__ __forceinline__ typename Store<T>::V create_ship(const AstroParams &p, const CreateDraws<S> &d, bool second,
+                                                           float is, float ic, T &b_out) {
+    const float u0 = float(d.u_out[0]) - 0.5f;
+    const float u1 = float(d.u_out[1]) - 0.5f;
+    const float o0 = p.outer_pos * (u0 > 0.0f ? 1.0f : (u0 < 0.0f ? -1.0f : 0.0f));
+    const float o1 = p.outer_pos * (u1 > 0.0f ? 1.0f : (u1 < 0.0f ? -1.0f : 0.0f));
+    const float i0 = p.inner_pos * is, i1 = p.inner_pos * ic;
+    const bool outer_first = d.u_choice < 0.5;
+    float sx, sy;
+    if (d.n == 1) {
+        sx = second ? -o0 : o0;
+        sy = second ? -o1 : o1;
+    } else {
+        const bool outer = second ? !outer_first : outer_first;
+        sx = outer ? o0 : i0;
+        sy = outer ? o1 : i1;
+    }
+    b_out = T(6.2831855f * float(second ? d.u_bear[S - 1] : d.u_bear[0]));
+    typename Store<T>::V v;
+    v.x = T(sx);
+    v.y = T(sy);
+    v.z = T(0);
+    v.w = T(0);
+    return v;
+}
+
+// planet j of an n-planet game: position angle (sn, cs), velocity angle (vs, vc)
+template <typename T>
+__device__ __forceinline__ typename Store<T>::V create_planet(const AstroParams &p, int n, float sn, float cs,
+                                                             float vs, float vc) {
+    typename Store<T>::V v;
+    if (n <= 1) {
+        v.x = v.y = v.z = v.w = T(0);
+    } else {
+        const double amp = sqrt(p.gravity * p.planet_mass * double(n - 1) / 2.0);
+        v.x = T(p.planet_orbit * sn);
+        v.y = T(p.planet_orbit * cs);
+        v.z = T(amp * double(vs));
+        v.w = T(amp * double(vc));
+    }
+    return v;
+}
+
 // create() of one env spread over a row of 16 lanes, for PMAX <= 7: each
 // lane evaluates ONE direction() -- planet u's position angle (u < PMAX),
 // planet u - PMAX's velocity angle, or the inner ship slot's (u = 2 PMAX) --
@@ -1531,7 +1578,6 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
     using V = typename Store<T>::V;
     const size_t N = size_t(st.n_env);
     int n = d.n;
-    const bool many = n > 1;
     const double stp = TWO_PI / double(n);
     const double base = TWO_PI * d.u_base;
     const double turn = double(d.reverse) * PI / 2.0;
@@ -1546,44 +1592,15 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
     const float vs = __shfl(sn, vsrc, 64), vc = __shfl(cs, vsrc, 64);
 
     // ships (core.py:93-109): lane u < S writes ship u
-    const float u0 = float(d.u_out[0]) - 0.5f;
-    const float u1 = float(d.u_out[1]) - 0.5f;
-    const float o0 = p.outer_pos * (u0 > 0.0f ? 1.0f : (u0 < 0.0f ? -1.0f : 0.0f));
-    const float o1 = p.outer_pos * (u1 > 0.0f ? 1.0f : (u1 < 0.0f ? -1.0f : 0.0f));
-    const float i0 = p.inner_pos * is, i1 = p.inner_pos * ic;
-    const bool outer_first = d.u_choice < 0.5;
-    const bool second = S == 2 && u == 1;
-    float sx, sy;
-    if (n == 1) {
-        sx = second ? -o0 : o0;
-        sy = second ? -o1 : o1;
-    } else {
-        const bool outer = second ? !outer_first : outer_first;
-        sx = outer ? o0 : i0;
-        sy = outer ? o1 : i1;
-    }
-    const float b = 6.2831855f * float(second ? d.u_bear[S - 1] : d.u_bear[0]);
+    T b;
+    const V sv = create_ship<T, S>(p, d, S == 2 && u == 1, is, ic, b);
     if (write && u < S) {
-        V v;
-        v.x = T(sx);
-        v.y = T(sy);
-        v.z = T(0);
-        v.w = T(0);
-        reinterpret_cast<V *>(st.ships)[size_t(u) * N + ie] = v;
-        reinterpret_cast<T *>(st.ships_b)[size_t(u) * N + ie] = T(b);
+        reinterpret_cast<V *>(st.ships)[size_t(u) * N + ie] = sv;
+        reinterpret_cast<T *>(st.ships_b)[size_t(u) * N + ie] = b;
     }
     // planets (core.py:111-121): lane j < n writes planet j
     if (write && u < PMAX) {
-        V v;
-        if (!many) {
-            v.x = v.y = v.z = v.w = T(0);
-        } else {
-            const double amp = sqrt(p.gravity * p.planet_mass * double(n - 1) / 2.0);
-            v.x = T(p.planet_orbit * sn);
-            v.y = T(p.planet_orbit * cs);
-            v.z = T(amp * double(vs));
-            v.w = T(amp * double(vc));
-        }
+        const V v = create_planet<T>(p, n, sn, cs, vs, vc);
         if (u < n) reinterpret_cast<V *>(st.planets)[size_t(u) * N + ie] = v;
     }
     if (n > PMAX) n = PMAX;
@@ -2967,7 +2984,10 @@ template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false, b
 #ifndef ASTRO_P8_WAVES
 #define ASTRO_P8_WAVES 3   // 8 planet slots: 141 VGPRs, no spills (4 waves: 128 VGPRs, 41 spilled; c5 34.3 -> 31.1 us)
 #endif
-__global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : 4)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+#ifndef ASTRO_P4_WAVES
+#define ASTRO_P4_WAVES 3   // 4 planet slots without helpers: 135 VGPRs, no spills (4 waves: 128 VGPRs, 7 spilled;
+#endif                     // c3 at 1M envs 139.6 -> 127.1 us, at 256k 39.5 -> 37.3 us, ab_p4_waves.jsonl)
+__global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? 2 : (PMAX > 4 ? ASTRO_P8_WAVES : ASTRO_P4_WAVES)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {

@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 WL=${WL:-c3}
 OUT=gpurun_out/r3prof/$WL
 mkdir -p $OUT
-ARGS="--workload $WL --no-cpu ${EXTRA_ARGS:-}"
+ARGS="--workload $WL --no-cpu --no-single --no-features --steps ${PSTEPS:-300} ${EXTRA_ARGS:-}"
 run() {
   local tag=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace "$@" -d $OUT/$tag -o run -f csv -- python bench.py $ARGS > $OUT/$tag.log 2>&1
@@ -31,3 +31,10 @@ if [ "${REQ:-1}" = 1 ]; then   # request sizes: the bytes behind FETCH_SIZE / WR
   run wrreq --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
 fi
 PROFILE_SCRIPT=tools/profile_r3.sh python3 tools/prof_summary.py $OUT $WL
+rc=$?
+du -sh $OUT/* | sort -h | tail -4
+# keep the summaries, drop rocprofv3's raw per-dispatch files (gpurun returns at most 64 MiB)
+for d in stats fetch write insts rdreq wrreq; do
+  [ -d $OUT/$d ] && find $OUT/$d -type f ! -name 'run_kernel_stats.csv' -delete
+done
+exit $rc
