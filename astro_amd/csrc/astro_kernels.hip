@@ -1422,6 +1422,34 @@ __device__ __forceinline__ double pair_swap(double v) {
     return __longlong_as_double((long long)(uint32_t(lo)) | ((long long)hi << 32));
 }
 
+// Within each 16-lane row of the wave (the reset pass's rows), by DPP:
+// lane K of the row to the whole row (row_newbcast), and lane (u + R) mod 16
+// to lane u (row_ror:16-R).  A DPP move instead of an LDS-routed ds_bpermute.
+template <int K>
+__device__ __forceinline__ int row_bcast_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false);
+}
+template <int K>
+__device__ __forceinline__ float row_bcast(float v) {
+    return __int_as_float(row_bcast_i<K>(__float_as_int(v)));
+}
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = row_bcast_i<K>(int(b & 0xffffffffll));
+    const int hi = row_bcast_i<K>(int(b >> 32));
+    return __longlong_as_double((long long)(uint32_t(lo)) | ((long long)hi << 32));
+}
+template <int R>
+__device__ __forceinline__ int row_from_i(int v) {   // lane u of the row reads lane (u + R) mod 16
+    static_assert(R > 0 && R < 16, "row rotation");
+    return __builtin_amdgcn_update_dpp(0, v, 0x120 + (16 - R), 0xf, 0xf, false);
+}
+template <int R>
+__device__ __forceinline__ float row_from(float v) {
+    return __int_as_float(row_from_i<R>(__float_as_int(v)));
+}
+
 // OR of a per-lane flag over the lane's group (all group lanes must be active)
 template <int LPE = 4>
 __device__ __forceinline__ bool quad_any(bool f, int lane) {
@@ -1587,9 +1615,8 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
     ang = u == 2 * PMAX ? float(TWO_PI * d.u_inner) : ang;
     float sn, cs;
     np_sincosf(ang, sn, cs);
-    const float is = __shfl(sn, row0 | (2 * PMAX), 64), ic = __shfl(cs, row0 | (2 * PMAX), 64);
-    const int vsrc = row0 | (PMAX + (u < PMAX ? u : 0));
-    const float vs = __shfl(sn, vsrc, 64), vc = __shfl(cs, vsrc, 64);
+    const float is = row_bcast<2 * PMAX>(sn), ic = row_bcast<2 * PMAX>(cs);
+    const float vs = row_from<PMAX>(sn), vc = row_from<PMAX>(cs);   // (lanes u < PMAX: lane PMAX + u's)
 
     // ships (core.py:93-109): lane u < S writes ship u
     T b;
@@ -1681,24 +1708,25 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     mask |= mask >> 4;
     mask |= mask >> 8;
     mask |= mask >> 16;
-    const uint32_t v = uint32_t(__shfl(int(w), row0, 64)) & mask;
+    const uint32_t v = uint32_t(row_bcast_i<0>(int(w))) & mask;
     const bool fast = !ud && rng != 0 && v <= rng && (p.planets_only == 0 || int(v) + 1 == p.planets_only);
     // lane k of the row: R_k = rand() of outputs k, k + 1
-    const uint32_t wn = uint32_t(__shfl(int(w), row0 | ((u + 1) & 15), 64));
+    const uint32_t wn = uint32_t(row_from_i<1>(int(w)));
     const double R = rand53(w, wn);
     CreateDraws<S> d;
     d.n = 1 + int(v);
     const bool many = d.n > 1;
-    d.u_out[0] = __shfl(R, row0 | 1, 64);
-    d.u_out[1] = __shfl(R, row0 | 3, 64);
-    d.u_inner = __shfl(R, row0 | 5, 64);
+    d.u_out[0] = row_bcast<1>(R);
+    d.u_out[1] = row_bcast<3>(R);
+    d.u_inner = row_bcast<5>(R);
     // (every shuffle unconditional: its source lane must be active)
-    const double r_choice = __shfl(R, row0 | 7, 64);
-    const double r_base = __shfl(R, row0 | (9 + 2 * S), 64);
-    const uint32_t w_rev = uint32_t(__shfl(int(w), row0 | (11 + 2 * S), 64));
+    const double r_choice = row_bcast<7>(R);
+    const double r_base = row_bcast<9 + 2 * S>(R);
+    const uint32_t w_rev = uint32_t(row_bcast_i<11 + 2 * S>(int(w)));
     d.u_choice = many ? r_choice : 1.0;
 #pragma unroll
-    for (int s = 0; s < S; ++s) d.u_bear[s] = __shfl(R, row0 | ((many ? 9 : 7) + 2 * s), 64);
+    for (int s = 0; s < S; ++s) d.u_bear[s] = many ? (s == 0 ? row_bcast<9>(R) : row_bcast<11>(R))
+                                                   : (s == 0 ? r_choice : row_bcast<9>(R));
     d.u_base = many ? r_base : 0.0;
     d.reverse = many && (w_rev & 1u) == 0 ? -1 : 1;
     d.exhausted = false;   // NW outputs, far below the 227 the lazy generator covers
@@ -2520,6 +2548,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     //      S), control, own planet slots (read whether live or not; padding
     //      is masked below)
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
+#ifdef ASTRO_HDR_FIRST   // A/B: the header before any other load leaves
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     const V sv = ships[size_t(sq) * NN + i];
     const T sbv = ships_b[size_t(sq) * NN + i];
     int ctl = tick_control<S>(drv, i, sq, NN, kt);
