@@ -2327,6 +2327,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // (wave_sync syncs one wave whenever the build's QW > 1, whatever this instance's WPG)
     static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, wave-scoped LDS sync");
     constexpr bool PENDING_ON_HELPER = HELP && (ASTRO_PENDING_ON_HELPER == 2 || (ASTRO_PENDING_ON_HELPER == 1 && LPE == 4));
+    // the planet update on the helpers: pair instance only (the quad instance
+    // of c2 lost with it there: 5.08 -> 5.33 us, ab_quad_planets_on_helper.jsonl)
+    constexpr bool PLANETS_ON_HELPER = HELP && LPE == 2;
     const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
     const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
     float4 (*s_body)[NBOD2] = s_body_all[wv];
@@ -2414,7 +2417,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             // step wave (the survivors' stored after the post; the step wave
             // then skips it: c3 12.39 -> 11.92 us with eight step waves per
             // workgroup; the quad instance of config 2 keeps it, 5.45 vs 5.50)
-            constexpr bool PLANETS = LPE == 2;
+            constexpr bool PLANETS = PLANETS_ON_HELPER;
             const size_t NN = size_t(N);
             V *planets = reinterpret_cast<V *>(st.planets);
             constexpr int PPL = PMAX / LPE;
@@ -2548,9 +2551,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     //      S), control, own planet slots (read whether live or not; padding
     //      is masked below)
     const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
-#ifdef ASTRO_HDR_FIRST   // A/B: the header before any other load leaves
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     const V sv = ships[size_t(sq) * NN + i];
     const T sbv = ships_b[size_t(sq) * NN + i];
     int ctl = tick_control<S>(drv, i, sq, NN, kt);
@@ -2895,7 +2895,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 
             STAMP(6);
             // ---- own planets (core.py:289-294); the pair instance's helper waves do it
-            if constexpr (!(HELP && LPE == 2)) {
+            if constexpr (!PLANETS_ON_HELPER) {
                 V pout[PPL];
                 planet_update<T, S, PMAX, LPE, PPL>(p, pv, mpx, mpy, q, np, t0, slot_last, pout);
 #pragma unroll

@@ -368,9 +368,9 @@ def main():
     if graphs:
         # The K launches' GPU time without the host's submission: the same
         # graphs replayed once more right after the region, the stream kept
-        # busy by a ~100 us spin kernel while the host submits them, the
-        # events around the replays only (ROCm has no event nodes in graphs)
-        torch.cuda._sleep(200000)
+        # busy by a ~1 ms spin kernel while the host submits them, the events
+        # around the replays only (ROCm has no event nodes in graphs)
+        torch.cuda._sleep(2000000)
         g0e, g1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         g0e.record(stream)
         for g in graphs:
@@ -496,7 +496,7 @@ def main():
                 sw, hw = env.launch_waves()
                 per_simd = sw / 1024.0
                 frac_i = rate / peak
-                note = ('%d step waves (%.2f per SIMD)%s; %s' % (
+                note = ('%d step waves (%.2f launched per SIMD)%s; %s' % (
                     sw, per_simd, (' + %d helper waves' % hw) if hw else '',
                     'issue-bound' if frac_i > 0.8 else
                     ('partly issue-bound: VALU issue %.0f%% of peak, the rest latency (DESIGN.md section 3)' % (

@@ -52,7 +52,8 @@ def main():
     tag = dict(n_env=b['config']['n_env_per_gpu'], kernel=b['roofline']['kernel'],
                lanes_per_env=b['roofline']['lanes_per_env'],
                mean_live_bullets=b['stats']['mean_live_bullets'], resets_per_step=b['stats']['resets_per_step'],
-               command='python bench.py --workload %s --no-cpu (%s)' % (wl, os.environ.get('PROFILE_SCRIPT', 'tools/profile_r2.sh')))
+               command='python bench.py %s (%s)' % (os.environ.get('PROFILE_ARGS', '--workload %s --no-cpu' % wl),
+                                                   os.environ.get('PROFILE_SCRIPT', 'tools/profile_r2.sh')))
     tag['kernel'] = {1: 'lane', 2: 'pair', 4: 'quad'}[tag['lanes_per_env']]
     f, nf = counters(os.path.join(out, 'fetch', 'run_counter_collection.csv'))
     w, nw = counters(os.path.join(out, 'write', 'run_counter_collection.csv'))

@@ -30,7 +30,7 @@ if [ "${REQ:-1}" = 1 ]; then   # request sizes: the bytes behind FETCH_SIZE / WR
   run rdreq --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
   run wrreq --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
 fi
-PROFILE_SCRIPT=tools/profile_r3.sh python3 tools/prof_summary.py $OUT $WL
+PROFILE_ARGS="$ARGS" PROFILE_SCRIPT=tools/profile_r3.sh python3 tools/prof_summary.py $OUT $WL
 rc=$?
 du -sh $OUT/* | sort -h | tail -4
 # keep the summaries, drop rocprofv3's raw per-dispatch files (gpurun returns at most 64 MiB)
