@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B timing of library builds on the bench's own timed region (hipGraph
-replays of 100 astro_step launches, c3 by default), interleaved over rounds
-so clock drift hits every build alike.
+replays of 100 astro_step launches, c3 by default, after the bench's
+300-tick burn-in; before round 3's last A/Bs there was none, so games were
+young), interleaved over rounds so clock drift hits every build alike.
 
     python tools/ab.py --libs libastro_hip,libastro_hip_var[:kernel] [--workload c3] [--rounds 5]
 """
@@ -28,6 +29,8 @@ def make(spec, wl, n, ticks, rollout):
     env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=w['b_cap'],
                      p_pad=w['p_pad'], auto_reset=True, kernel=kernel or 'auto', planets_only=w['planets_only'])
     env.reset()
+    if rollout > 0:   # age the batch as bench.py does (games of every age, bullets in flight)
+        env.rollout(rollout, 'random', tick0=1 << 40, stats=False)
     ctl = torch.from_numpy(bench.controls(0, n, env.S, ticks)).cuda()
     for t in range(50):
         env.launch(ctl[t].data_ptr())
@@ -50,6 +53,7 @@ def main():
     ap.add_argument('--n-env', type=int, default=0)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--burn-in', type=int, default=300, help='random-policy rollout ticks after reset (bench.py: 300)')
     a = ap.parse_args()
     libs = a.libs.split(',')
     n = a.n_env or bench.WORKLOADS[a.workload]['n']
@@ -57,7 +61,7 @@ def main():
     rolls = {l: [] for l in libs}
     for r in range(a.rounds):
         for lib in libs:
-            env, g = make(lib, a.workload, n, 150, 0)
+            env, g = make(lib, a.workload, n, 150, a.burn_in)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
