@@ -85,17 +85,20 @@ class _Arena:
             self.host = None
 
 
-# ASTRO_SHIM=mapped: the game's arrays in host memory the kernel addresses
-# directly; default 'copy' (measured faster on MI355X: a kernel's dependent
-# loads over PCIe cost more than two small copies, profiles/round3/)
-SHIM_MODE = os.environ.get('ASTRO_SHIM', 'copy')
+# The single-game arena: 'mapped' (default) = the game's arrays in host
+# memory the kernel addresses directly, a tick is one launch and one event;
+# ASTRO_SHIM=copy = a device arena with one packed H2D and one packed D2H copy
+# per tick.  Measured on MI355X (bench.py `single_game`): mapped 35-40 us per
+# core.step, copy 43-53 us
+SHIM_MODE = os.environ.get('ASTRO_SHIM', 'mapped')
 
 
 class _Shim:
     """One float64 game on the device for the single-game surface: its
     arrays packed in one buffer (_Arena), a tick = the input written into
-    the host view, one H2D copy, one launch, one D2H copy, one wait for an
-    event (busy-polled: a blocking synchronisation wakes ~10-30 us late)."""
+    the host view, one launch (mapped; copy mode: between one H2D and one D2H
+    copy of the packed arena), one wait for an event (busy-polled: a blocking
+    synchronisation wakes ~10-30 us late)."""
 
     def __init__(self, config, b_cap, device, mode=None):
         self.env = env = BatchedEnv(config, 1, device=device, b_cap=b_cap, dtype=torch.float64,

@@ -123,16 +123,18 @@ def single_game_latency(cfg, ticks=2000, seed=0):
     """The single-game drop-in (astro_amd.core, what astro/server.py's
     game_tick and core.play's loop call): us per core.step tick with random
     controls, re-creating on termination, and us per tick of core.play with
-    two random bots (Bots.control + step + Tick bookkeeping); the shim's
-    default ('copy') and its host-mapped variant."""
+    two random bots (Bots.control + step + Tick bookkeeping); both arena
+    modes of the shim, the default's numbers as the line's."""
     from astro_amd import core
+    default = core.SHIM_MODE
     out = {}
-    for mode in ('mapped', 'copy'):   # (the default last: its numbers are the line's)
+    for mode in sorted(('mapped', 'copy'), key=lambda m: m == default):   # (the default last)
         core._ENVS.clear()
         core.SHIM_MODE = mode
         out.update(_single_game(core, cfg, ticks, seed))
         out['us_per_step_' + mode] = out['us_per_step']
-    core.SHIM_MODE = os.environ.get('ASTRO_SHIM', 'copy')
+    out['mode'] = default
+    core.SHIM_MODE = default
     core._ENVS.clear()
     return out
 
@@ -163,9 +165,10 @@ def _single_game(core, cfg, ticks, seed):
     dp = time.perf_counter() - t1
     return dict(us_per_step=dt / ticks * 1e6, steps=ticks, creates=n_create, us_per_play_tick=dp / played * 1e6,
                 play_ticks=played, games=k,
-                path='astro_amd.core.step (float64 state, bit-exact to the reference): per tick one H2D copy of '
-                     'the packed state, one launch, one D2H copy, one busy-polled event; "mapped": the state in '
-                     'host memory the kernel addresses directly, no copies')
+                path='astro_amd.core.step (float64 state, bit-exact to the reference): "mapped" (default): the '
+                     'game in host memory the kernel addresses directly, one launch and one busy-polled event per '
+                     'tick; "copy": one H2D copy of the packed state, one launch, one D2H copy, one event; the CPU '
+                     'reference port (oracle/port.py) per tick on one core beside it')
 
 
 def _free_port():
@@ -364,7 +367,7 @@ def main():
     barrier()
     s1 = env.stat_dict()
     gpu_ms_stream = ev0.elapsed_time(ev1) / args.steps
-    gpu_ms_per_step, gpu_timing = gpu_ms_stream, 'hipEvent pair on the stream around the timed region / K'
+    gpu_ms_graph = None
     if graphs:
         # The K launches' GPU time without the host's submission: the same
         # graphs replayed once more right after the region, the stream kept
@@ -377,10 +380,23 @@ def main():
             g.replay()
         g1e.record(stream)
         torch.cuda.synchronize(dev)
-        gpu_ms_per_step = g0e.elapsed_time(g1e) / (args.steps - head)
-        gpu_timing = ('the timed region\'s %d graph-captured launches replayed once more right after it, back to back '
-                      'behind a spin kernel (so the host has submitted them): hipEvent pair / %d'
-                      % (args.steps - head, args.steps - head))
+        gpu_ms_graph = g0e.elapsed_time(g1e) / (args.steps - head)
+    # The launches' GPU time as the kernels run back to back: the K launches
+    # issued eagerly (each its own AQL packet, no graph) behind a spin kernel
+    # long enough for the host to submit them all, an event pair around them.
+    # A graph replay adds ~15-20 us per graph on the GPU timeline (first node
+    # behind the previous work), which a 20-launch run cannot amortise.
+    torch.cuda._sleep(int(2e6 + 4e4 * args.steps))
+    q0e, q1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    q0e.record(stream)
+    for k in range(args.steps):
+        env.launch(ptrs[args.warmup + k])
+    q1e.record(stream)
+    torch.cuda.synchronize(dev)
+    gpu_ms_per_step = q0e.elapsed_time(q1e) / args.steps
+    gpu_timing = ('%d launches issued back to back behind a spin kernel long enough for the host to submit them '
+                  'all (right after the timed region, continuing its games): hipEvent pair / %d'
+                  % (args.steps, args.steps))
     dev_err = env.device_errors()
 
     # Kernel duration: launches timed one by one (hipEvent pair around each,
@@ -526,6 +542,7 @@ def main():
                           timing=gpu_timing),
             issue_roofline=issue,
             gpu_ms_per_step=gpu_ms_per_step, gpu_ms_per_step_stream_events=gpu_ms_stream,
+            gpu_ms_per_step_graph_replay=gpu_ms_graph,
             timed_region='%d launches: %d eager, then %s' % (
                 args.steps, head, ('%d hipGraph replay(s) of up to %d launches, each graph replayed once '
                                    'untimed before the region' % (len(graphs), args.graph)) if graphs else 'no graph'),

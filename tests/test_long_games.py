@@ -127,12 +127,18 @@ def _roll(state, i):
 # ------------------------------------------------------------------ GPU
 
 @pytest.mark.gpu
-def test_config1_trace_through_hip_shim():
+@pytest.mark.parametrize('mode', ['mapped', 'copy'])
+def test_config1_trace_through_hip_shim(mode, monkeypatch):
     """BASELINE config 1 through the drop-in surface: astro_amd.core.create /
     step (one float64 env on the HIP kernel) reproduce the reference's
-    1000-tick trace bit for bit, re-creates included."""
+    1000-tick trace bit for bit, re-creates included -- with the game's arena
+    in host-mapped memory (the default) and in device memory with copies."""
     from astro_amd import core
+    monkeypatch.setattr(core, 'SHIM_MODE', mode)
+    monkeypatch.setattr(core, '_ENVS', {})
     _run_config1(lambda: core.create(DEFAULT_CONFIG), lambda s, c: core.step(s, c, DEFAULT_CONFIG))
+    sh = next(iter(core._ENVS.values()))
+    assert sh.arena.mode == mode
 
 
 @pytest.mark.gpu

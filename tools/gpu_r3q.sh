@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r3q
+O=gpurun_out/r3q2
 mkdir -p $O
 step() {
   local name=$1 limit=$2; shift 2
