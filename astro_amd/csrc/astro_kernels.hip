@@ -657,9 +657,10 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, con
 // Env i's generate_configs stream (core.py:77-83): RandomState(stream_seed)
 // .randint(1 << 30) = one masked MT word per game.  The stream record holds
 // the MTStream cursor (x_k, x_{k+397}, k; the ring beside it) and the CURRENT
-// game's seed; the next game's seed is drawn one game ahead and lives in hdr
-// (.z) with key[397] of its init chain (.w, valid with KEY_VALID), so a
-// reset can start creating before the cold stream record arrives.
+// game's seed; the next game's seed is drawn by the game's first step (hdr .z
+// is UNDRAWN until then) and lives in hdr (.z) with key[397] of its init
+// chain (.w, valid with KEY_VALID), so a reset can start creating before the
+// cold stream record arrives and never touches the cursor itself.
 
 // Start env i's next game: its seed was drawn one game ahead (hdr word 2) and
 // key[397] of that seed fetched from the key table by an earlier step (hdr
@@ -1960,6 +1961,9 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
 // survivors; the step waves only write words 0-1.  1: quad instance only
 // (its step waves are the critical path: c2 5.36 -> 5.20 us A/B), 2: pair
 // too (there the helpers' resets are the tail: c3 12.19 -> 12.52 us), 0: off
+#ifndef ASTRO_HELPER_PRIO
+#define ASTRO_HELPER_PRIO 0
+#endif
 #ifndef ASTRO_PENDING_ON_HELPER
 #define ASTRO_PENDING_ON_HELPER 1
 #endif
@@ -2488,6 +2492,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 return QuadCounts{};
             }
             asm volatile("" ::: "memory");
+#if ASTRO_HELPER_PRIO > 0   // A/B: the helper's reset pass wins issue arbitration after the post
+            __builtin_amdgcn_s_setprio(ASTRO_HELPER_PRIO);
+#endif
 #ifdef ASTRO_STAMPS
             asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[20])::"memory");
 #endif
