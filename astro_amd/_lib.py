@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # (ASTRO_LIB: another build of the same library, e.g. an A/B variant from tools/build_var.sh)
 LIB_PATH = os.environ.get('ASTRO_LIB') or os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
@@ -92,6 +92,9 @@ _SYMBOLS = {
     'astro_step': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    'astro_step_many': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
+                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     'astro_reset': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'astro_stream_init': (ctypes.c_int, [ctypes.POINTER(AstroState), ctypes.c_void_p,

@@ -3533,6 +3533,25 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
     return dispatch<StepL>(*p, *s, drv, reward, done, stats, int(auto_reset), reinterpret_cast<hipStream_t>(stream));
 }
 
+int astro_step_many(const AstroParams *p, const AstroState *s, const int8_t *control, int32_t k, float *reward,
+                    uint8_t *done, uint64_t *stats, int32_t auto_reset, void *stream) {
+    if (k < 0) return fail(-35, "k must be >= 0");
+    if (k == 0) return 0;
+    int rc = astro_step(p, s, control, reward, done, stats, auto_reset, stream);   // checks the arguments
+    if (rc || s->n_env == 0) return rc;
+    const size_t per = size_t(s->n_env) * size_t(p->nships);
+    TickDriver drv{};
+    drv.policy = ASTRO_POLICY_CONTROL;
+    drv.ticks = 1;
+    for (int32_t t = 1; t < k; ++t) {
+        drv.control = control + size_t(t) * per;
+        rc = dispatch<StepL>(*p, *s, drv, reward + size_t(t) * per, done + size_t(t) * size_t(s->n_env), stats,
+                             int(auto_reset), reinterpret_cast<hipStream_t>(stream));
+        if (rc) return rc;
+    }
+    return 0;
+}
+
 int astro_rollout(const AstroParams *p, const AstroState *s, const AstroPolicy *policy, int32_t ticks,
                   const int8_t *control, float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset,
                   void *stream) {

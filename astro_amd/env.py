@@ -187,6 +187,35 @@ class BatchedEnv:
         self._last = (self.reward, self.done)
         return self.obs(), self.reward, self.done
 
+    def step_many(self, controls, auto_reset=None, stats=True):
+        """k consecutive steps with the controls given up front (int8
+        [k, N, S]): k launches of the one-tick kernel from C
+        (astro_step_many).  Returns (reward f32 [k, N, S], done u8 [k, N]);
+        identical to k step() calls."""
+        c = controls
+        if not (torch.is_tensor(c) and c.dtype == torch.int8 and c.device == self.device
+                and c.is_contiguous()):
+            c = torch.as_tensor(c, device=self.device).to(torch.int8).contiguous()
+        if c.dim() != 3 or c.shape[1:] != (self.n_env, self.S):
+            raise ValueError('controls must be [k, %d, %d], got %s' % (self.n_env, self.S, tuple(c.shape)))
+        k = c.shape[0]
+        reward = torch.empty(k, self.n_env, self.S, dtype=torch.float32, device=self.device)
+        done = torch.empty(k, self.n_env, dtype=torch.uint8, device=self.device)
+        self.launch_many(c.data_ptr(), k, reward.data_ptr(), done.data_ptr(), auto_reset, stats)
+        if k:
+            self._last = (reward[-1], done[-1])
+        return reward, done
+
+    def launch_many(self, control_ptr, k, reward_ptr, done_ptr, auto_reset=None, stats=True, stream=None):
+        """Raw astro_step_many (no checks, no allocation): for timed loops."""
+        ar = self.auto_reset if auto_reset is None else bool(auto_reset)
+        rc = self.lib.astro_step_many(
+            ctypes.byref(self.params), ctypes.byref(self.state), control_ptr, int(k), reward_ptr, done_ptr,
+            self.stats.data_ptr() if stats else None, 1 if ar else 0,
+            stream if stream is not None else _stream_ptr(self.device))
+        if rc != 0:
+            _lib.check(rc, 'astro_step_many')
+
     def launch(self, control_ptr, auto_reset=None, stats=True, stream=None):
         """Raw launch (no checks, no allocation): for timed loops/graphs."""
         ar = self.auto_reset if auto_reset is None else bool(auto_reset)

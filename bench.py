@@ -268,6 +268,9 @@ def main():
                     help='secondary line: the workload as K-tick rollouts with the on-device random '
                          'policy, K ticks per launch (0 = skip)')
     ap.add_argument('--no-features', action='store_true', help='skip the observation-builder line')
+    ap.add_argument('--launcher', default='graph', choices=['graph', 'c'],
+                    help='timed region: hipGraph replays of the captured launches, or the K launches issued '
+                         'from C (astro_step_many)')
     ap.add_argument('--eager-head', type=int, default=0,
                     help='timed launches issued eagerly before the graph replays: the GPU runs them while the '
                          'host submits the first graph (~10-40 us), so it does not idle at the start of the region')
@@ -336,7 +339,12 @@ def main():
     # before the region: its first replay uploads it.
     head = min(args.steps, max(0, args.eager_head)) if args.graph > 0 else args.steps
     graphs = []
-    if args.graph > 0 and head < args.steps:
+    use_c = args.launcher == 'c'
+    if use_c:   # the K launches issued from C (astro_step_many), per-tick outputs
+        head = 0
+        rew_k = torch.empty(args.steps, n, env.S, dtype=torch.float32, device=dev)
+        done_k = torch.empty(args.steps, n, dtype=torch.uint8, device=dev)
+    if args.graph > 0 and head < args.steps and not use_c:
         cap = torch.cuda.Stream(dev)
         cap.wait_stream(stream)
         with torch.cuda.stream(cap):
@@ -355,6 +363,8 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    if use_c:
+        env.launch_many(ptrs[args.warmup], args.steps, rew_k.data_ptr(), done_k.data_ptr())
     for k in range(head):
         env.launch(ptrs[args.warmup + k])
     for g in graphs:
@@ -543,7 +553,8 @@ def main():
             issue_roofline=issue,
             gpu_ms_per_step=gpu_ms_per_step, gpu_ms_per_step_stream_events=gpu_ms_stream,
             gpu_ms_per_step_graph_replay=gpu_ms_graph,
-            timed_region='%d launches: %d eager, then %s' % (
+            timed_region=('%d launches issued from C in one astro_step_many call' % args.steps) if use_c else
+                         '%d launches: %d eager, then %s' % (
                 args.steps, head, ('%d hipGraph replay(s) of up to %d launches, each graph replayed once '
                                    'untimed before the region' % (len(graphs), args.graph)) if graphs else 'no graph'),
             burn_in_ticks=args.burn_in, settle_launches=settle,

@@ -7,6 +7,7 @@
  * reference interface, batched over n_env independent games:
  *
  *   astro_step         <- core.step(state, control, config)  core.py:215-303
+ *   astro_step_many    <- k calls of core.step with controls known ahead
  *   astro_rollout      <- core.play's tick loop with Bots.control (core.py:359-410)
  *                         for open-loop / scripted controls, K ticks per launch
  *                         (plus auto-reset = core.create(next config of the
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 15
+#define ASTRO_ABI_VERSION 16
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -191,6 +192,15 @@ const char *astro_last_error(void);
 int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
                float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset,
                void *stream);
+
+/* k consecutive astro_step calls with controls given up front -- k launches
+ * of the one-tick kernel issued from C, arguments checked once: control
+ * int8 [k][n_env][nships], reward float [k][n_env][nships], done uint8
+ * [k][n_env].  Identical results to k astro_step calls (and to astro_rollout
+ * with ASTRO_POLICY_CONTROL, which fuses the k ticks into one launch); for
+ * a host loop that has its controls ahead but wants each tick's launch. */
+int astro_step_many(const AstroParams *p, const AstroState *s, const int8_t *control, int32_t k,
+                    float *reward, uint8_t *done, uint64_t *stats, int32_t auto_reset, void *stream);
 
 /* `ticks` consecutive ticks (each exactly astro_step with auto_reset as
  * given), controls from `policy`: reward float [ticks][n_env][nships], done

@@ -613,6 +613,30 @@ def test_rollout_equals_stepping(kernel, dtype):
 
 
 @pytest.mark.parametrize('kernel', KERNELS)
+def test_step_many_equals_stepping(kernel):
+    """step_many(controls [K, N, S]) (astro_step_many: K one-tick launches
+    issued from C) == K calls of step(controls[k]) bit for bit, auto-reset
+    and the helper-wave instance included; K = 0 changes nothing."""
+    cfg = CFG['rapid']
+    n, K = 700, 23
+    a = _env(cfg, n, dtype=torch.float32, b_cap=24, p_pad=4, auto_reset=True, kernel=kernel)
+    b = _env(cfg, n, dtype=torch.float32, b_cap=24, p_pad=4, auto_reset=True, kernel=kernel)
+    a.reset()
+    b.reset()
+    ctl = torch.from_numpy(np.random.RandomState(5).randint(0, 6, size=(K, n, 2)).astype(np.int8)).cuda()
+    r0, d0 = a.step_many(ctl[:0])
+    assert r0.shape == (0, n, 2) and d0.shape == (0, n)
+    rew, done = a.step_many(ctl)
+    for k in range(K):
+        _, r, d = b.step(ctl[k])
+        assert torch.equal(rew[k], r) and torch.equal(done[k], d), k
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert a.stat_dict() == b.stat_dict()
+    a.check_errors()
+
+
+@pytest.mark.parametrize('kernel', KERNELS)
 def test_rollout_device_policies(kernel):
     """The on-device RANDOM policy draws bench.py's controls (global env id,
     tick); NOTHING is script.NothingBot's constant 2."""

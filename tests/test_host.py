@@ -31,7 +31,7 @@ def _declared_functions():
 
 def test_library_exports_every_header_symbol(lib):
     names = _declared_functions()
-    assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_reset',
+    assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_step_many', 'astro_reset',
                           'astro_stream_init', 'astro_keytable_build', 'astro_features', 'astro_rollout',
                           'astro_controls', 'astro_host_alloc', 'astro_host_free'}
     out = subprocess.check_output(['nm', '-D', '--defined-only', _lib.LIB_PATH], text=True)
@@ -73,6 +73,11 @@ def test_argument_validation_without_gpu(lib):
     p.p_pad = 17
     rc = lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None)
     assert rc == -13
+    rc = lib.astro_step_many(ctypes.byref(p), ctypes.byref(s), None, -1, None, None, None, 0, None)
+    assert rc == -35 and b'k must be' in lib.astro_last_error()
+    assert lib.astro_step_many(ctypes.byref(p), ctypes.byref(s), None, 0, None, None, None, 0, None) == 0
+    rc = lib.astro_step_many(ctypes.byref(p), ctypes.byref(s), None, 3, None, None, None, 0, None)
+    assert rc == -13   # checked as astro_step is
     p.p_pad = 4
     p.planets_only = 5   # > max_planets
     assert lib.astro_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None) == -19
