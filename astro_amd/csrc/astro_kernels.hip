@@ -3648,6 +3648,36 @@ int astro_host_free(void *host) {
     return e == hipSuccess ? 0 : fail(-1000 - int(e), "hipHostFree failed: %s", hipGetErrorString(e));
 }
 
+int astro_dev_alloc(uint64_t bytes, int32_t kind, void **device) {
+    if (!device) return fail(-82, "device is NULL");
+    *device = nullptr;
+    if (bytes == 0) return fail(-81, "bytes must be > 0");
+    unsigned flags;
+    switch (kind) {
+    case ASTRO_MEM_DEFAULT: flags = hipDeviceMallocDefault; break;
+    case ASTRO_MEM_FINEGRAINED: flags = hipDeviceMallocFinegrained; break;
+    case ASTRO_MEM_UNCACHED: flags = hipDeviceMallocUncached; break;
+    default: return fail(-83, "kind must be ASTRO_MEM_DEFAULT, _FINEGRAINED or _UNCACHED (got %d)", int(kind));
+    }
+    void *d = nullptr;
+    hipError_t e = hipExtMallocWithFlags(&d, size_t(bytes), flags);
+    if (e != hipSuccess) return fail(-1000 - int(e), "hipExtMallocWithFlags(%llu, %u) failed: %s",
+                                     (unsigned long long)bytes, flags, hipGetErrorString(e));
+    e = hipMemset(d, 0, size_t(bytes));
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return fail(-1000 - int(e), "hipMemset failed: %s", hipGetErrorString(e));
+    }
+    *device = d;
+    return 0;
+}
+
+int astro_dev_free(void *device) {
+    if (!device) return 0;
+    const hipError_t e = hipFree(device);
+    return e == hipSuccess ? 0 : fail(-1000 - int(e), "hipFree failed: %s", hipGetErrorString(e));
+}
+
 int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_t rows, void *stream) {
     int rc = check_params(p);
     if (rc) return rc;

@@ -27,6 +27,7 @@ current torch stream.  There is no CPU path.
 """
 import collections
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -69,6 +70,38 @@ def key_table(device):
 
 QUAD_MAX_ENVS = 32768   # include/astro_step.h ASTRO_QUAD_MAX_ENVS
 
+_TORCH_TYPESTR = {torch.float32: '<f4', torch.float64: '<f8', torch.int32: '<i4', torch.uint8: '|u1'}
+
+
+class _DevBlock:
+    """One astro_dev_alloc block, seen by torch through the CUDA array
+    interface (the tensors keep the block alive; freed with the last)."""
+
+    def __init__(self, lib, shape, dtype, kind):
+        self.lib = lib
+        n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+        ptr = ctypes.c_void_p()
+        _lib.check(lib.astro_dev_alloc(max(n, 16), kind, ctypes.byref(ptr)), 'astro_dev_alloc')
+        self.ptr = ptr.value
+        self.__cuda_array_interface__ = dict(shape=tuple(int(x) for x in shape), typestr=_TORCH_TYPESTR[dtype],
+                                             data=(self.ptr, False), version=2, strides=None)
+
+    def __del__(self):
+        if getattr(self, 'ptr', None):
+            self.lib.astro_dev_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def _dev_tensor(lib, shape, dtype, device, kind):
+    """A zeroed device tensor in memory of the given ASTRO_MEM_* kind."""
+    if kind == _lib.MEM['default']:
+        return torch.zeros(shape, dtype=dtype, device=device)
+    with torch.cuda.device(device):
+        t = torch.as_tensor(_DevBlock(lib, shape, dtype, kind), device=device)
+    if t.data_ptr() == 0 or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+        raise RuntimeError('astro_dev_alloc block not seen as a %s %s tensor' % (dtype, tuple(shape)))
+    return t
+
 
 class BatchedEnv:
     """N lockstep games of one Config on one device.
@@ -88,11 +121,15 @@ class BatchedEnv:
                   filtered to the seeds whose create() draws exactly P planets
                   (config.generate_configs_filtered); max_planets must be a
                   power of two
+    mem        -- memory kind of the per-step state arrays (ships, ships_b,
+                  planets, bullets, hdr, reward, done): 'default' (hipMalloc),
+                  'uncached' or 'finegrained' (astro_dev_alloc); default: the
+                  ASTRO_MEM environment variable, else 'default'
     """
 
     def __init__(self, config, n_env, device=None, b_cap=32, p_pad=None,
                  dtype=torch.float32, env_offset=0, auto_reset=True, kernel='auto',
-                 use_key_table=True, planets_only=0):
+                 use_key_table=True, planets_only=0, mem=None):
         _schedule.check_config(config)
         planets_only = int(planets_only)
         if planets_only and (not 1 <= planets_only <= config.max_planets
@@ -118,14 +155,18 @@ class BatchedEnv:
         self.schedule = _schedule.build(config)
 
         N, S, dev = self.n_env, self.S, self.device
+        self.mem = mem or os.environ.get('ASTRO_MEM', 'default')
+        if self.mem not in _lib.MEM:
+            raise ValueError('mem must be one of %s' % sorted(_lib.MEM))
         z = lambda *shape, dt=dtype: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
-        self.ships = z(S, N, 4)
-        self.ships_b = z(S, N)
-        self.planets = z(self.p_pad, N, 4)
-        self.bullets = z(N, self.b_cap, 4)
-        self.hdr = z(N, 4, dt=torch.int32)
-        self.reward = z(N, S, dt=torch.float32)
-        self.done = z(N, dt=torch.uint8)
+        zs = lambda *shape, dt=dtype: _dev_tensor(self.lib, shape, dt, dev, _lib.MEM[self.mem])  # noqa: E731
+        self.ships = zs(S, N, 4)
+        self.ships_b = zs(S, N)
+        self.planets = zs(self.p_pad, N, 4)
+        self.bullets = zs(N, self.b_cap, 4)
+        self.hdr = zs(N, 4, dt=torch.int32)
+        self.reward = zs(N, S, dt=torch.float32)
+        self.done = zs(N, dt=torch.uint8)
         self.errors = z(1, dt=torch.int32)   # AstroState.errors: the ASTRO_ERR_* bits a faulting launch sets
         self.stream = z(N, 4, dt=torch.int32)
         self.stream_ring = z(N, MT_N, dt=torch.int32)

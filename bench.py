@@ -274,6 +274,9 @@ def main():
     ap.add_argument('--eager-head', type=int, default=0,
                     help='timed launches issued eagerly before the graph replays: the GPU runs them while the '
                          'host submits the first graph (~10-40 us), so it does not idle at the start of the region')
+    ap.add_argument('--end-poll', default='event', choices=['event', 'stream'],
+                    help="how the host sees the region's end before its synchronize: busy-poll an event "
+                         "recorded behind the launches, or busy-poll the stream itself (no event in the region)")
     ap.add_argument('--no-single', action='store_true', help='skip the single-game drop-in latency line')
     ap.add_argument('--stub', action='store_true', help=argparse.SUPPRESS)   # launcher test: no GPU work
     args = ap.parse_args()
@@ -361,22 +364,28 @@ def main():
     s0 = env.stat_dict()
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    poll_event = args.end_poll == 'event'
     t0 = time.perf_counter()
-    ev0.record(stream)
+    if poll_event:
+        ev0.record(stream)
     if use_c:
         env.launch_many(ptrs[args.warmup], args.steps, rew_k.data_ptr(), done_k.data_ptr())
     for k in range(head):
         env.launch(ptrs[args.warmup + k])
     for g in graphs:
         g.replay()
-    ev1.record(stream)
-    while not ev1.query():   # (busy-poll the end: a blocking wait wakes ~10 us late)
-        pass
+    if poll_event:
+        ev1.record(stream)
+        while not ev1.query():   # (busy-poll the end: a blocking wait wakes ~10 us late)
+            pass
+    else:
+        while not stream.query():
+            pass
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     barrier()
     s1 = env.stat_dict()
-    gpu_ms_stream = ev0.elapsed_time(ev1) / args.steps
+    gpu_ms_stream = ev0.elapsed_time(ev1) / args.steps if poll_event else None
     gpu_ms_graph = None
     if graphs:
         # The K launches' GPU time without the host's submission: the same

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 16
+#define ASTRO_ABI_VERSION 17
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -250,6 +250,22 @@ int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_
  * Every kernel access crosses PCIe: for one or a few games only. */
 int astro_host_alloc(uint64_t bytes, void **host, void **device);
 int astro_host_free(void *host);
+
+/* Device memory of a chosen kind, zeroed, for the per-step state arrays
+ * (ships, ships_b, planets, bullets, hdr, reward, done).  A launch reads each
+ * of them once and writes each once, so the L2 only holds what the end of
+ * the launch must write back:
+ *   ASTRO_MEM_DEFAULT     hipMalloc (coarse-grained, cached in L2)
+ *   ASTRO_MEM_FINEGRAINED hipDeviceMallocFinegrained
+ *   ASTRO_MEM_UNCACHED    hipDeviceMallocUncached (L2 bypassed: stores go
+ *                         straight to the memory side, nothing is left
+ *                         dirty at the end of a launch)
+ * Free with astro_dev_free. */
+#define ASTRO_MEM_DEFAULT 0
+#define ASTRO_MEM_FINEGRAINED 1
+#define ASTRO_MEM_UNCACHED 2
+int astro_dev_alloc(uint64_t bytes, int32_t kind, void **device);
+int astro_dev_free(void *device);
 
 #ifdef __cplusplus
 }

@@ -33,7 +33,8 @@ def test_library_exports_every_header_symbol(lib):
     names = _declared_functions()
     assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_step_many', 'astro_reset',
                           'astro_stream_init', 'astro_keytable_build', 'astro_features', 'astro_rollout',
-                          'astro_controls', 'astro_host_alloc', 'astro_host_free'}
+                          'astro_controls', 'astro_host_alloc', 'astro_host_free', 'astro_dev_alloc',
+                          'astro_dev_free'}
     out = subprocess.check_output(['nm', '-D', '--defined-only', _lib.LIB_PATH], text=True)
     exported = set(re.findall(r' T (astro_\w+)$', out, re.M))
     assert set(names) <= exported
@@ -117,6 +118,10 @@ def test_argument_validation_without_gpu(lib):
     assert lib.astro_host_alloc(0, ctypes.byref(h), ctypes.byref(d)) == -81
     assert lib.astro_host_alloc(64, None, None) == -80
     assert lib.astro_host_free(None) == 0
+    assert lib.astro_dev_alloc(0, 0, ctypes.byref(d)) == -81
+    assert lib.astro_dev_alloc(64, 0, None) == -82
+    assert lib.astro_dev_alloc(64, 3, ctypes.byref(d)) == -83
+    assert lib.astro_dev_free(None) == 0
     assert lib.astro_keytable_build(None, 0, 16, None) == -50
     assert lib.astro_keytable_build(ctypes.c_void_p(16), (1 << 30) - 8, 16, None) == -51
 
