@@ -94,7 +94,7 @@ class _DevBlock:
 
 def _dev_tensor(lib, shape, dtype, device, kind):
     """A zeroed device tensor in memory of the given ASTRO_MEM_* kind."""
-    if kind == _lib.MEM['default']:
+    if kind == _lib.MEM['default'] or 0 in shape:
         return torch.zeros(shape, dtype=dtype, device=device)
     with torch.cuda.device(device):
         t = torch.as_tensor(_DevBlock(lib, shape, dtype, kind), device=device)
