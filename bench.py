@@ -274,6 +274,9 @@ def main():
     ap.add_argument('--eager-head', type=int, default=0,
                     help='timed launches issued eagerly before the graph replays: the GPU runs them while the '
                          'host submits the first graph (~10-40 us), so it does not idle at the start of the region')
+    ap.add_argument('--replay', default='torch', choices=['torch', 'raw'],
+                    help="how the timed region replays a captured graph: torch's CUDAGraph.replay(), or "
+                         "hipGraphLaunch on its executable graph directly (no per-replay wrapper)")
     ap.add_argument('--end-poll', default='event', choices=['event', 'stream'],
                     help="how the host sees the region's end before its synchronize: busy-poll an event "
                          "recorded behind the launches, or busy-poll the stream itself (no event in the region)")
@@ -365,6 +368,24 @@ def main():
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     poll_event = args.end_poll == 'event'
+    replays = [g.replay for g in graphs]
+    if args.replay == 'raw' and graphs:
+        # hipGraphLaunch of the HIP runtime the library (and torch) runs on,
+        # resolved through the library's own dependency
+        import ctypes
+        hgl = env.lib.hipGraphLaunch
+        hgl.restype, hgl.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
+        sp = ctypes.c_void_p(stream.cuda_stream)
+
+        def raw(ge):
+            ge = ctypes.c_void_p(ge)
+
+            def launch():
+                rc = hgl(ge, sp)
+                if rc != 0:
+                    raise RuntimeError('hipGraphLaunch returned %d' % rc)
+            return launch
+        replays = [raw(g.raw_cuda_graph_exec()) for g in graphs]
     t0 = time.perf_counter()
     if poll_event:
         ev0.record(stream)
@@ -372,8 +393,8 @@ def main():
         env.launch_many(ptrs[args.warmup], args.steps, rew_k.data_ptr(), done_k.data_ptr())
     for k in range(head):
         env.launch(ptrs[args.warmup + k])
-    for g in graphs:
-        g.replay()
+    for r in replays:
+        r()
     if poll_event:
         ev1.record(stream)
         while not ev1.query():   # (busy-poll the end: a blocking wait wakes ~10 us late)
