@@ -14,6 +14,7 @@ env id, tick) and resident in HBM before the timed region.  Rank 0 prints
 one JSON line; value = env-steps of ALL ranks / max-over-ranks wall time.
 """
 import argparse
+import ctypes
 import json
 import multiprocessing as mp
 import os
@@ -365,11 +366,15 @@ def main():
                 graphs.append(g)
         stream.wait_stream(cap)
         replays = [g.replay for g in graphs]
+        hgl = None
         if args.replay == 'raw' and graphs:
             # hipGraphLaunch of the HIP runtime the library (and torch) runs on,
             # resolved through the library's own dependency
-            import ctypes
-            hgl = env.lib.hipGraphLaunch
+            try:
+                hgl = env.lib.hipGraphLaunch
+            except AttributeError:   # (not resolvable: torch's replay, and the line says so)
+                args.replay = 'torch'
+        if hgl is not None:
             hgl.restype, hgl.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
             sp = ctypes.c_void_p(stream.cuda_stream)
 
