@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # (ASTRO_LIB: another build of the same library, e.g. an A/B variant from tools/build_var.sh)
 LIB_PATH = os.environ.get('ASTRO_LIB') or os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
@@ -18,8 +18,7 @@ NSTATS = 8
 KERNELS = {'auto': 0, 'lane': 1, 'quad': 2, 'pair': 3}
 MEM = {'default': 0, 'finegrained': 1, 'uncached': 2}   # include/astro_step.h ASTRO_MEM_*
 ERRORS = {1: 'a helper wave never saw its step wave post (its finished games were not re-created)',
-          2: "a step wave never saw its helper's header read",
-          4: "a step wave never saw its helper's bullet pass"}
+          2: "a step wave never saw its helper's header read"}
 
 
 class AstroParams(ctypes.Structure):

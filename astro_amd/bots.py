@@ -8,9 +8,11 @@ EGO view of a state (``core.roll_ships``: the bot's own ship first), as
 
 Arithmetic follows the reference's numpy expressions one to one, so with the
 state's own dtypes (float32 arrays for a fresh game, float64 after) a
-decision is the reference's decision (tests/test_bots.py: every golden state,
-both ships).  For batched rollouts use the device policies
-(``BatchedEnv.step(policy=...)``), not these per-game objects.
+decision is the reference's decision (tests/test_bots_logs.py
+test_scriptbot_decisions_match_reference: every golden state, both ships).
+For batched play use the device policies -- ``BatchedEnv.rollout(ticks,
+policy)``, ``BatchedEnv.controls(policy)`` and ``BatchedEnv.play(bots)`` --
+not these per-game objects.
 """
 import numpy as np
 

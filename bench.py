@@ -120,6 +120,24 @@ def algorithmic_bytes(env, dstats, launches):
     return (fixed + var) / launches
 
 
+def aggregate_roofline(bytes_all_ranks, steps, wall_max, n_dev):
+    """Whole-job HBM roofline: every rank's section 8(d) bytes per launch,
+    summed, times the launches, over the slowest rank's wall time, against
+    the peak of the distinct GPUs behind the ranks."""
+    peak = HBM_PEAK_GBS * max(1, n_dev)
+    achieved = bytes_all_ranks * steps / wall_max / 1e9 if wall_max > 0 else 0.0
+    return dict(achieved=achieved, peak=peak, unit='GB/s', frac=achieved / peak, n_gpus=n_dev,
+                basis='sum over ranks of bytes per launch x launches / max-over-ranks wall (host clock, '
+                      'the timed region)')
+
+
+def add_cpu_baseline(out, wl, args):
+    """The CPU baseline fields of the line (rank 0, after the GPU work)."""
+    procs = args.cpu_procs or cpu_share()
+    out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, procs, wl['planets_only'])
+    out['speedup_vs_cpu'] = out['value'] / out['cpu_baseline']['value'] if out['value'] else None
+
+
 def single_game_latency(cfg, ticks=2000, seed=0):
     """The single-game drop-in (astro_amd.core, what astro/server.py's
     game_tick and core.play's loop call): us per core.step tick with random
@@ -137,6 +155,13 @@ def single_game_latency(cfg, ticks=2000, seed=0):
     out['mode'] = default
     core.SHIM_MODE = default
     core._ENVS.clear()
+    # the CPU comparison for this same path: oracle/port.py's core.step on
+    # one host core, the same config, random controls, re-create on termination
+    from oracle import port
+    steps, secs = port.run_for(cfg, 2.0, seed=seed)
+    out['cpu_port_us_per_step'] = secs / steps * 1e6
+    out['cpu_port_sample'] = '%d core.step ticks of oracle/port.py on one host core, %s' % (
+        steps, 'DEFAULT_CONFIG' if cfg == DEFAULT_CONFIG else 'the same config')
     return out
 
 
@@ -222,12 +247,18 @@ def stub_rank(args, world, rank):
         dist.barrier()
     wall = _shard.max_over_ranks(0.001 * (1 + rank))
     n_ranks = int(_shard.sum_over_ranks([1])[0])
-    if rank == 0:
-        print(json.dumps(dict(metric=METRIC, value=0.0, unit='env-steps/s', n_gpus=0, ranks=n_ranks,
-                              steps=args.steps, warmup=args.warmup, ms_per_step=wall / max(1, args.steps) * 1e3,
-                              higher_is_better=True, scaling='weak', vs_baseline=None, stub=True)), flush=True)
+    bytes_all = float(_shard.sum_over_ranks([1000.0])[0])
     if world > 1:
         dist.destroy_process_group()
+    if rank == 0:
+        out = dict(metric=METRIC, value=0.0, unit='env-steps/s', n_gpus=0, ranks=n_ranks,
+                   steps=args.steps, warmup=args.warmup, ms_per_step=wall / max(1, args.steps) * 1e3,
+                   higher_is_better=True, scaling='weak', vs_baseline=None, stub=True,
+                   roofline=dict(bound='hbm', achieved=0.0, peak=HBM_PEAK_GBS, unit='GB/s', frac=0.0, traffic=None,
+                                 scope='stub', aggregate=aggregate_roofline(bytes_all, args.steps, wall, n_ranks)))
+        if not args.no_cpu:
+            add_cpu_baseline(out, WORKLOADS[args.workload], args)
+        print(json.dumps(out), flush=True)
 
 
 PROFILE_ROUNDS = ('round3', 'round2')
@@ -392,11 +423,18 @@ def main():
         # keep the GPU busy for --warm-ms before the region, continuing the
         # games with the same graphs: on a box that idled before this process
         # the first short region ran at 20 us per step on the GPU's own
-        # timeline, the next ones at 13 (profiles/round3s2/bench_c3_20_reps.jsonl)
+        # timeline, the next ones at 13 (profiles/round3s2/bench_c3_20_reps.jsonl).
+        # Bounded on the GPU's progress, not the host's: each round of replays
+        # is waited for before the next is queued, so at most one round is
+        # in flight when the time is up
         t_w = time.perf_counter()
+        ev_w = torch.cuda.Event()
         while time.perf_counter() - t_w < args.warm_ms * 1e-3:
             for r in replays:
                 r()
+            ev_w.record(stream)
+            while not ev_w.query():
+                pass
     barrier()
     s0 = env.stat_dict()
     barrier()
@@ -420,8 +458,10 @@ def main():
             pass
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    # faults of the timed region (read before stat_dict, which raises on them)
+    dev_err = env.device_errors(clear=False)
     barrier()
-    s1 = env.stat_dict()
+    s1 = env.stat_dict() if not dev_err else dict(s0)
     gpu_ms_stream = ev0.elapsed_time(ev1) / args.steps if poll_event else None
     gpu_ms_graph = None
     if graphs:
@@ -453,7 +493,6 @@ def main():
     gpu_timing = ('%d launches issued back to back behind a spin kernel long enough for the host to submit them '
                   'all (right after the timed region, continuing its games): hipEvent pair / %d'
                   % (args.steps, args.steps))
-    dev_err = env.device_errors()
 
     # Kernel duration: launches timed one by one (hipEvent pair around each,
     # on the launch stream), continuing the same games with fresh controls.
@@ -466,6 +505,8 @@ def main():
         b.record(stream)
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    # every launch since the region: the GPU-time replays and the calibration
+    dev_err |= env.device_errors()
 
     # Secondary lines (not the headline `value`).  (1) The same workload as
     # K-tick rollouts: controls from the on-device splitmix64 policy (the
@@ -509,6 +550,7 @@ def main():
             kernel='astro_features_kernel', shape=list(out_f.shape), ms=fms,
             write_GBps=fbytes / (fms * 1e-3) / 1e9, hbm_frac=fbytes / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS)
 
+    dev_err |= env.device_errors()   # (the secondary lines' launches)
     wall_max = _shard.max_over_ranks(wall, device=red_dev)
     d = {k: s1[k] - s0[k] for k in s0}
     fl = env.flags
@@ -519,6 +561,8 @@ def main():
     # distinct devices behind the ranks (a one-GPU rehearsal shares one)
     n_dev = int(_shard.sum_over_ranks([1 if local < torch.cuda.device_count() else 0], device=red_dev)[0])
     bytes_launch = algorithmic_bytes(env, d, args.steps)
+    # every rank's section 8(d) bytes per launch, summed: the aggregate roofline
+    bytes_all = float(_shard.sum_over_ranks([bytes_launch], device=red_dev)[0])
 
     if rank == 0:
         n_total = n * world
@@ -591,6 +635,9 @@ def main():
                         state=args.state, parallelism='env-shard x%d (no collectives)' % world),
             roofline=dict(bound='hbm', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
                           frac=achieved / HBM_PEAK_GBS, traffic=traffic,
+                          scope=('per GPU: rank 0\'s dominant kernel on its own GPU' if world > 1
+                                 else 'the one GPU\'s dominant kernel'),
+                          aggregate=aggregate_roofline(bytes_all, args.steps, wall_max, n_dev),
                           bytes_per_launch=bytes_launch, kernel_ms=launch_ms,
                           kernel_ms_eager_event_pairs=kern_ms,
                           kernel=('astro_step_kernel' if env.step_kernel == 'lane' else 'astro_step_quad_kernel'),
@@ -616,21 +663,21 @@ def main():
                        envs_flag_overflow=tot[5], envs_flag_create_exhausted=tot[6]),
         )
         out.update(extras)
-        if world == 1 and not args.no_single:
+        if not args.no_single:   # (rank 0's own GPU; every rank is past the GPU region)
             out['single_game'] = single_game_latency(DEFAULT_CONFIG)
-        if world == 1 and not args.no_cpu:
-            procs = args.cpu_procs or cpu_share()
-            out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, procs, wl['planets_only'])
-            out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']
-            if 'single_game' in out:   # the port's own per-tick time, one core
-                out['single_game']['cpu_port_us_per_step'] = 1e6 / out['cpu_baseline']['per_core']
+    # rank 0's host-side lines run after every rank has left the GPU region
+    # (the last collective above): the CPU baseline of the same workload, on
+    # this rank's CPU share, for any number of ranks
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    if rank == 0:
+        if not args.no_cpu:
+            add_cpu_baseline(out, wl, args)
         print(json.dumps(out), flush=True)
         if int(tot[7]):
             raise SystemExit('bench: a launch reported device error bits (device_errors=%d): the state '
                              'and the line above are not trusted' % int(tot[7]))
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
 
 
 if __name__ == '__main__':

@@ -20,8 +20,11 @@
  *                         (rl.py:36-112), the observation a policy consumes
  *
  * Conventions
- *   - The caller owns and allocates all device memory (e.g. PyTorch
- *     tensors); the library never allocates, frees or synchronises.
+ *   - The caller owns all memory the entry points read and write (e.g.
+ *     PyTorch tensors): astro_step/rollout/reset/... never allocate, free or
+ *     synchronise.  The only allocating calls are the optional helpers
+ *     astro_host_alloc / astro_dev_alloc (and their frees), which hand the
+ *     caller memory of a particular kind to own.
  *   - Every call is stream-ordered and asynchronous on `stream` (a
  *     hipStream_t passed as void*, NULL = the null stream).
  *   - Return 0 on success, a negative code on a bad argument (-1..-99) or a
@@ -29,8 +32,8 @@
  *     last failure of the calling thread.
  *   - Ships and planets are struct-of-arrays, entity-major: slot s of env i
  *     lives at [s * n_env + i], so consecutive lanes (envs) touch consecutive
- *     bytes; bullets are one contiguous row per env.  Element type is float
- *     (state_f64 = 0) or double (state_f64 = 1).
+ *     bytes; bullets are packed per bullet group of 16 envs (AstroState).
+ *     Element type is float (state_f64 = 0) or double (state_f64 = 1).
  */
 #ifndef ASTRO_STEP_H
 #define ASTRO_STEP_H
@@ -41,7 +44,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 17
+#define ASTRO_ABI_VERSION 18
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -67,7 +70,7 @@ typedef struct AstroParams {
     int32_t solo;
     int32_t max_planets;   /* create(): 1..max_planets planets */
     int32_t p_pad;         /* planet slots per env, 1..16 (>= max_planets) */
-    int32_t b_cap;         /* bullet slots per env, 1..65535 */
+    int32_t b_cap;         /* live bullets an env may hold, 1..ASTRO_MAX_B_CAP */
     int32_t timeout_tick;  /* first tick k with max_time <= t_k + dt */
     const uint32_t *fire_bits; /* device: bit k = fire on tick k, k < timeout_tick */
     int32_t kernel;        /* ASTRO_KERNEL_AUTO / _LANE / _QUAD / _PAIR (results are identical) */
@@ -90,9 +93,15 @@ typedef struct AstroParams {
 enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2, ASTRO_KERNEL_PAIR = 3 };
 #define ASTRO_QUAD_MAX_ENVS 32768
 
+#define ASTRO_MAX_B_CAP 1000
+#define ASTRO_BULLET_GROUP 16
+
 /* Per-env state arrays (device pointers).  hdr packs
  *   hdr[4*i+0] = tick (steps since create, < 2^22)
- *   hdr[4*i+1] = nplanets | flags << 8 | nbullets << 16
+ *   hdr[4*i+1] = nplanets (5 bits) | flags << 5 (2 bits) | half << 7 |
+ *                nbullets << 8 (10 bits) | boff << 18 (14 bits): the env's live
+ *                bullets are entries [boff, boff + nbullets) of its bullet
+ *                group's region in bullet half `half` (see `bullets`)
  *   hdr[4*i+2] = the NEXT game's seed (drawn one game ahead from the stream,
  *                < 2^30) | key_valid << 31, or undrawn << 30 alone: a game's
  *                create leaves the draw to its first step, off the reset path
@@ -106,7 +115,15 @@ typedef struct AstroState {
     void *ships;        /* [nships][n_env][4]  x, y, dx, dy */
     void *ships_b;      /* [nships][n_env]     bearing */
     void *planets;      /* [p_pad][n_env][4]   x, y, dx, dy */
-    void *bullets;      /* [n_env][b_cap][4]   x, y, dx, dy (one contiguous row per env) */
+    void *bullets;      /* [2][n_env * (b_cap + nships)][4]  x, y, dx, dy: two halves.  Envs
+                           16g .. 16g+15 (a bullet group) keep their live bullets in
+                           the group's region of a half, entries from 16g * (b_cap +
+                           nships) on, one env after the other (hdr: half, boff,
+                           nbullets; every env of a group is in the same half).  A step
+                           reads a group from its half and writes it to the other;
+                           astro_reset keeps the half.  Entries between envs' bullets
+                           are unused.  Zeroed hdr words 1 (or astro_stream_init) =
+                           half 0, no bullets. */
     int32_t *hdr;       /* [n_env][4], 16-byte aligned */
     uint32_t *stream;   /* [n_env][4] generate_configs cursor: x_k, x_{k+397}, k, current game's seed
                            (x = the MT19937 word sequence of the env's RandomState, core.py:79) */
@@ -125,8 +142,7 @@ typedef struct AstroState {
 enum {
     ASTRO_ERR_HELPER_WAIT = 1,  /* a helper wave's wait for its step wave's post expired:
                                    that wave's finished games were not re-created */
-    ASTRO_ERR_HEADER_WAIT = 2,  /* a step wave's wait for its helper's header read expired */
-    ASTRO_ERR_BULLETS_WAIT = 4  /* a step wave's wait for its helper's bullet pass expired */
+    ASTRO_ERR_HEADER_WAIT = 2   /* a step wave's wait for its helper's header read expired */
 };
 
 /* Control sources of astro_rollout / astro_controls. */

@@ -25,7 +25,7 @@ def _run(args, extra_env=None):
 
 
 def test_self_launched_ranks_print_one_line():
-    p, lines = _run(['--gpus', '2', '--steps', '7', '--stub'])
+    p, lines = _run(['--gpus', '2', '--steps', '7', '--stub', '--no-cpu'])
     assert p.returncode == 0, p.stderr
     assert len(lines) == 1, p.stdout
     j = json.loads(lines[0])
@@ -34,11 +34,27 @@ def test_self_launched_ranks_print_one_line():
     assert abs(j['ms_per_step'] - 2.0 / 7) < 1e-9
 
 
+def test_multi_rank_line_carries_roofline_and_cpu_baseline():
+    """BASELINE.json's metric is 'at 1/2/4/8 MI355X vs CPU core.step': a
+    2-rank line carries the per-GPU roofline with an aggregate over ranks and
+    the CPU baseline (rank 0, after every rank left the GPU region), through
+    the same code path as a real rank."""
+    p, lines = _run(['--gpus', '2', '--steps', '5', '--stub', '--cpu-seconds', '0.3', '--cpu-procs', '1'])
+    assert p.returncode == 0, p.stderr
+    j = json.loads(lines[0])
+    assert {'roofline', 'cpu_baseline'} <= set(j)
+    agg = j['roofline']['aggregate']
+    # 2 ranks x 1000 stub bytes per launch x 5 launches / max wall (2 ms)
+    assert abs(agg['achieved'] - 2 * 1000 * 5 / 0.002 / 1e9) < 1e-12
+    cb = j['cpu_baseline']
+    assert cb['cores'] == 1 and cb['kind'] == 'port' and cb['value'] > 0
+
+
 def test_four_ranks_and_single_rank():
-    p, lines = _run(['--gpus', '4', '--stub'])
+    p, lines = _run(['--gpus', '4', '--stub', '--no-cpu'])
     assert p.returncode == 0, p.stderr
     assert len(lines) == 1 and json.loads(lines[0])['ranks'] == 4
-    p, lines = _run(['--gpus', '1', '--stub'])
+    p, lines = _run(['--gpus', '1', '--stub', '--no-cpu'])
     assert p.returncode == 0, p.stderr
     assert len(lines) == 1 and json.loads(lines[0])['ranks'] == 1
 
@@ -46,6 +62,6 @@ def test_four_ranks_and_single_rank():
 def test_failing_rank_ends_the_launch():
     """A rank that cannot join (bad backend name) fails the whole launch
     with a nonzero code instead of leaving the others waiting."""
-    p, lines = _run(['--gpus', '2', '--stub'], {'ASTRO_DIST_BACKEND': 'no-such-backend'})
+    p, lines = _run(['--gpus', '2', '--stub', '--no-cpu'], {'ASTRO_DIST_BACKEND': 'no-such-backend'})
     assert p.returncode != 0
     assert lines == []

@@ -406,7 +406,7 @@ def test_config4_eight_shards_compose():
         assert torch.equal(env.ships, full.ships[:, sl]), r
         assert torch.equal(env.ships_b, full.ships_b[:, sl]), r
         assert torch.equal(env.planets, full.planets[:, sl]), r
-        assert torch.equal(env.bullets, full.bullets[sl]), r
+        assert torch.equal(env.bullet_rows(), full.bullet_rows()[sl]), r   # (the packed halves differ in shape)
         del env
     assert int(full.stat_dict()['resets']) > 0
 
@@ -440,8 +440,9 @@ def test_config5_full_size_instances_agree():
     assert int(np_.min()) == 1 and int(np_.max()) == 8
     st = full.stat_dict()
     assert st['resets'] > 10000 and st['bullets_in'] > 0
-    arrays = ('hdr', 'stream', 'stream_ring', 'bullets')      # [N, ...]
+    arrays = ('hdr', 'stream', 'stream_ring')                 # [N, ...]
     slot_major = ('ships', 'ships_b', 'planets')              # [slot, N, ...]
+    rows = full.bullet_rows()
     for r in range(2):
         half = run(r * (n // 2), n // 2)
         assert half.launch_waves() == (2048, 2048)
@@ -450,9 +451,10 @@ def test_config5_full_size_instances_agree():
             assert torch.equal(getattr(half, f), getattr(full, f)[sl]), (r, f)
         for f in slot_major:
             assert torch.equal(getattr(half, f), getattr(full, f)[:, sl]), (r, f)
+        assert torch.equal(half.bullet_rows(), rows[sl]), r
         del half
     lane = run(0, n, kernel='lane')
-    for f in arrays + slot_major:
+    for f in arrays + slot_major + ('bullets',):   # same n: the packed halves too, holes included
         assert torch.equal(getattr(lane, f), getattr(full, f)), f
 
 

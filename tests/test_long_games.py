@@ -142,6 +142,51 @@ def test_config1_trace_through_hip_shim(mode, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_shim_two_threads_interleaved(monkeypatch):
+    """astro/server.py calls core.step from request threads: two games ticked
+    concurrently through the same shim arena (same config, the host-mapped
+    default) each stay their own game -- one thread replays config 1's
+    reference trace, the other plays seed 7 against the oracle port."""
+    import threading
+    from astro_amd import core
+    monkeypatch.setattr(core, '_ENVS', {})
+    errors = []
+
+    def trace():
+        try:
+            _run_config1(lambda: core.create(DEFAULT_CONFIG), lambda s, c: core.step(s, c, DEFAULT_CONFIG))
+        except Exception as e:   # (reported by the main thread)
+            errors.append(e)
+
+    def other():
+        try:
+            cfg = DEFAULT_CONFIG._replace(seed=7)
+            g = port.Game(cfg)
+            rng = np.random.RandomState(1)
+            st, want = core.create(cfg), g.create()
+            for t in range(1500):
+                ctl = rng.randint(0, 6, 2)
+                st, rew = core.step(st, ctl, cfg)
+                want, wrew = g.step(want, ctl)
+                assert np.array_equal(rew, wrew) and rew.dtype == wrew.dtype, t
+                if st is None:
+                    assert want is None, t
+                    st, want = core.create(cfg), g.create()
+                else:
+                    assert np.array_equal(st.ships.x, want.ships.x), t
+                    assert np.array_equal(st.bullets.x, want.bullets.x), t
+        except Exception as e:
+            errors.append(e)
+    th = [threading.Thread(target=f) for f in (trace, other)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    assert len(core._ENVS) == 1
+
+
+@pytest.mark.gpu
 def test_test_script_invariants_through_hip_shim():
     """test/test_core.py:88-98 on the HIP kernel: astro_amd.core.play with
     ScriptBot solo (max_time=20) -> winner 0; NothingBot vs ScriptBot ->
