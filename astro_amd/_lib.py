@@ -49,6 +49,8 @@ class AstroParams(ctypes.Structure):
         ('kernel', ctypes.c_int32),
         ('planets_only', ctypes.c_int32),
         ('key_table', ctypes.c_void_p),
+        ('fire_period', ctypes.c_int32),
+        ('fire_phase', ctypes.c_int32),
     ]
 
 

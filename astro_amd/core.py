@@ -136,6 +136,7 @@ class _Shim:
                 p = type(env.params).from_buffer_copy(env.params)
                 p.timeout_tick = tick if to else tick + 1
                 p.fire_bits = a.ptr('fire')
+                p.fire_period = 0   # (this call's fire word decides, not the config's periodic schedule)
                 self.params[tick, to] = p
 
     def stream(self):

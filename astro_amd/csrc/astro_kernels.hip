@@ -68,6 +68,30 @@ template <typename T> struct Store;
 template <> struct Store<float> { using V = F4; };
 template <> struct Store<double> { using V = D4; };
 
+// A state store of the step (A/B build -DASTRO_NT_STORES: nontemporal)
+template <typename X>
+__device__ __forceinline__ void st_out(X *p, const X &v) {
+#ifdef ASTRO_NT_STORES
+    if constexpr (sizeof(X) == 16 && alignof(X) == 16) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(*reinterpret_cast<const v4u *>(&v), reinterpret_cast<v4u *>(p));
+    } else if constexpr (sizeof(X) == 32) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(reinterpret_cast<const v4u *>(&v)[0], reinterpret_cast<v4u *>(p));
+        __builtin_nontemporal_store(reinterpret_cast<const v4u *>(&v)[1], reinterpret_cast<v4u *>(p) + 1);
+    } else if constexpr (sizeof(X) == 8) {
+        __builtin_nontemporal_store(*reinterpret_cast<const unsigned long long *>(&v),
+                                    reinterpret_cast<unsigned long long *>(p));
+    } else if constexpr (sizeof(X) == 4) {
+        __builtin_nontemporal_store(*reinterpret_cast<const unsigned *>(&v), reinterpret_cast<unsigned *>(p));
+    } else {
+        *p = v;
+    }
+#else
+    *p = v;
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // numpy 2.x float32 sin/cos (loops_trigonometric.dispatch.cpp): Cody-Waite
 // reduction + minimax polynomials, every multiply-add fused as numpy's
@@ -817,6 +841,17 @@ constexpr int NSTAMP = 24;   // 0-13 step sections, 14-15 placement, 16-19 reset
 
 constexpr int BLOCK = 64;
 
+// Does a game fire on this tick (core.py:262-280, the host's replay of the
+// float64 reload recurrence)?  A schedule that is exactly periodic (every
+// preset: the default fires on ticks 14 + 15k) is two kernel arguments and
+// costs no load; any other reads the fire bitmask -- a load keyed by the
+// header's tick, whose latency lands on whatever needs the answer first.
+__device__ __forceinline__ bool fires_at(const AstroParams &p, int tick, bool live) {
+    if (p.fire_period > 0) return live && uint32_t(tick) % uint32_t(p.fire_period) == uint32_t(p.fire_phase);
+    const uint32_t w = p.fire_bits[(live ? tick : 0) >> 5];
+    return live && ((w >> (tick & 31)) & 1u) != 0;
+}
+
 // Where a launch's controls come from and how many ticks it runs
 // (astro_step: one tick of a control array; astro_rollout: K ticks of a
 // control array or of an on-device policy).
@@ -1098,8 +1133,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
     const int half = hw1_half(hw);
     const int tick = int(uint32_t(h.x) & TICK_MASK);
     const bool live = tick < p.timeout_tick;
-    const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
-    const bool fires = ((fire_word >> (tick & 31)) & 1u) != 0;
+    const bool fires = fires_at(p, tick, live);
     const int nb = active ? min(hw1_nb(hw), p.b_cap) : 0;
     const int dst_off = row_incl_scan(nb + (active && fires ? S : 0)) - (nb + (active && fires ? S : 0));
 
@@ -2061,17 +2095,51 @@ __device__ __forceinline__ void report_error(const AstroState &st, uint32_t bits
 // bullets_rounds stages the envs' old bodies in LDS, collides, moves, culls
 // and compacts every live bullet into the other half, and leaves per env the
 // kept count (s_kept) and the ships the bullets hit (s_hit).
+// The wave's bullet groups (one for the quad kernel's 16 envs, two for the
+// pair kernel's 32): each group's region in the half it is read from and in
+// the half it is written to (wave-uniform; every env of a group is in the
+// same half)
+__device__ __forceinline__ size_t uniform64(size_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v)), hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+    return size_t(lo) | (size_t(hi) << 32);
+}
+
+struct BulletGroups {
+    // group 0's regions and group 1's minus group 0's: a select between
+    // two values (a select between two members became an indexed load from
+    // the struct in scratch memory)
+    size_t src0, dsrc, dst0, ddst;
+    __device__ __forceinline__ size_t src_of(uint32_t w) const {
+        return src0 + (bw_env(w) >= BGROUP ? dsrc : size_t(0)) + bw_pos(w);
+    }
+    __device__ __forceinline__ size_t dst_of(uint32_t w) const { return dst0 + (bw_env(w) >= BGROUP ? ddst : size_t(0)); }
+};
+
 template <typename T>
 struct BulletsIn {
-    int total, off, dst;
+    int total, off;
     uint32_t tag, bw0, bw1;
+    int half0, half1;   // (wave-uniform) the half each of the wave's bullet groups is read from
     typename Store<T>::V cur0, cur1;
 };
 
-// where bullet index word w's bullet is (source half) / goes (the other
-// half, after the env's `dst` first entries), in V entries from st.bullets
-__device__ __forceinline__ size_t bullet_src(const AstroState &st, const AstroParams &p, int base, uint32_t w) {
-    return bullet_base(st, p, bw_half(w), base + bw_env(w)) + size_t(bw_pos(w));
+// the wave's bullet groups' regions (recomputed where needed: scalar work,
+// cheaper than holding eight SGPRs across the physics)
+template <int LPE>
+__device__ __forceinline__ BulletGroups bullet_groups(const AstroState &st, const AstroParams &p, int base, int half0,
+                                                      int half1) {
+    BulletGroups g;
+    const size_t src0 = bullet_base(st, p, half0, base), dst0 = bullet_base(st, p, half0 ^ 1, base);
+    size_t dsrc = 0, ddst = 0;
+    if constexpr (64 / LPE > BGROUP) {   // (pair: the wave's second bullet group starts at env 16)
+        dsrc = bullet_base(st, p, half1, base + BGROUP) - src0;
+        ddst = bullet_base(st, p, half1 ^ 1, base + BGROUP) - dst0;
+    }
+    g.src0 = uniform64(src0);   // (wave-uniform: in SGPRs)
+    g.dsrc = uniform64(dsrc);
+    g.dst0 = uniform64(dst0);
+    g.ddst = uniform64(ddst);
+    return g;
 }
 
 template <typename T, int LPE>
@@ -2082,15 +2150,22 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroParams &p, cons
     using V = typename Store<T>::V;
     const V *bullets = reinterpret_cast<const V *>(st.bullets);
     BulletsIn<T> b;
-    // one scan for both: live bullets (low half) and live bullets + spawn
-    // slots (high half); a wave's sums are < 2^16 (nb <= b_cap <= 1000)
+    // one scan for both: the wave's live bullets (low half: their dense
+    // numbering) and, per bullet group, live bullets + the S spawn slots of
+    // the envs that fire this tick (high half: where each env's bullets go
+    // in the other half); a wave's sums are < 2^16 (nb <= b_cap <= 1000)
     const int v = q == 0 ? nb | ((nb + res) << 16) : 0;
     const int incl = wave_incl_scan(v, lane);
     b.off = (incl & 0xffff) - nb;
-    int dst = (incl >> 16) - (v >> 16);
-    if constexpr (64 / LPE > BGROUP)   // (pair: the wave's second bullet group starts at env 16)
+    int dst = (incl >> 16) - (nb + res);   // (every lane of the env)
+    // the wave's bullet groups, their halves and regions
+    b.half0 = __builtin_amdgcn_readfirstlane(hw1_half(hw));
+    b.half1 = b.half0;
+    if constexpr (64 / LPE > BGROUP) {   // (pair: the wave's second bullet group starts at env 16)
         dst -= e >= BGROUP ? (__builtin_amdgcn_readlane(incl, BGROUP * LPE - 1) >> 16) : 0;
-    b.dst = dst;
+        b.half1 = __builtin_amdgcn_readlane(hw1_half(hw), BGROUP * LPE);
+    }
+    const BulletGroups g = bullet_groups<LPE>(st, p, base, b.half0, b.half1);
 #ifdef ASTRO_ABLATE_BULLETS   // timing ablation only (wrong results)
     b.total = 0;
 #else
@@ -2112,8 +2187,8 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroParams &p, cons
     wave_sync();
     b.bw0 = lane < b.total ? s_index[lane] : 0u;
     b.bw1 = lane + 64 < min(b.total, QWIN) ? s_index[lane + 64] : 0u;
-    b.cur0 = bullets[bullet_src(st, p, base, b.bw0)];
-    b.cur1 = bullets[bullet_src(st, p, base, b.bw1)];
+    b.cur0 = bullets[g.src_of(b.bw0)];
+    b.cur1 = bullets[g.src_of(b.bw1)];
     return b;
 }
 
@@ -2137,6 +2212,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
     V *bullets = reinterpret_cast<V *>(st.bullets);
     const int total = b.total, off = b.off;
     const uint32_t tag = b.tag;
+    const BulletGroups g = bullet_groups<LPE>(st, p, base, b.half0, b.half1);
     uint32_t bw0 = b.bw0, bw1 = b.bw1;
     V cur0 = b.cur0, cur1 = b.cur1;
     if (total == 0) {   // uniform: nothing to do (bullets_begin left s_kept, s_hit cleared)
@@ -2172,8 +2248,8 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
               wave_sync();
               bw0 = w0 + lane < wend ? s_index[lane] : 0u;
               bw1 = w0 + 64 + lane < wend ? s_index[64 + lane] : 0u;
-              cur0 = bullets[bullet_src(st, p, base, bw0)];
-              cur1 = bullets[bullet_src(st, p, base, bw1)];
+              cur0 = bullets[g.src_of(bw0)];
+              cur1 = bullets[g.src_of(bw1)];
           }
           // one round: lane g takes live bullet r0 + g (index word bw, data cur)
           // NR rounds at once, lane g of round r taking live bullet r0 + 64 r + g
@@ -2303,9 +2379,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
                   const int first = lane - bw_slot(bws[r]);   // lane of the env's slot 0 (< 0: an earlier round)
                   const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
                   const int pos = kg - k0;
-                  if (kp)
-                      bullets[bullet_base(st, p, bw_half(bws[r]) ^ 1, base + be[r]) + size_t(s_dst[be[r]] + pos)] =
-                          out[r];
+                  if (kp) st_out(&bullets[g.dst_of(bws[r]) + size_t(s_dst[be[r]] + pos)], out[r]);
                   if (valid[r] && bw_last(bws[r])) s_kept[be[r]] = pos + int(kp);
                   carry = __builtin_amdgcn_readlane(k0, 63);
                   kept_before += __popcll(kb);
@@ -2324,7 +2398,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           constexpr int NR2 = PMAX <= 4 ? 2 : 1;
           if (nr >= 3) {
               bws[2] = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
-              curs[2] = bullets[bullet_src(st, p, base, bws[2])];
+              curs[2] = bullets[g.src_of(bws[2])];
           }
           if (nr >= 2) {
               rounds(std::integral_constant<int, NR2>(), w0, bws, curs);
@@ -2336,7 +2410,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           if (nr >= 3) rounds(std::integral_constant<int, 1>(), w0 + 128, bws + 2, curs + 2);
           for (int r0 = w0 + 192; r0 < wend; r0 += 64) {   // uniform; rare
               const uint32_t bw = r0 + lane < wend ? s_index[r0 + lane - w0] : 0u;
-              const V cur = bullets[bullet_src(st, p, base, bw)];
+              const V cur = bullets[g.src_of(bw)];
               rounds(std::integral_constant<int, 1>(), r0, &bw, &cur);
           }
         }
@@ -2356,8 +2430,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // LDS, one set per wave of the workgroup
     __shared__ float4 s_body_all[WPG][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
     __shared__ uint32_t s_index_all[WPG][QWIN];           // a window of the wave's live bullets, see bw_*
+    __shared__ int s_dst_all[WPG][QENV];                  // where each env's bullets go (bullets_begin)
     __shared__ int s_kept_all[WPG][QENV], s_hit_all[WPG][QENV], s_serial_all[WPG][QENV];
-    __shared__ int s_dst_all[WPG][QENV];                  // where each env's bullets go in the other half
     __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
     __shared__ HelpBox s_box_all[HELP ? WPG : 1];
     __shared__ uint32_t s_pre_all[HELP ? WPG : 1][HELP ? QENV : 1][2][13 + 2 * S];   // a helper's chains, made ahead
@@ -2369,6 +2443,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // step waves are the critical path (c2 5.36 -> 5.20 us A/B); in the pair
     // instance the helpers' resets are the tail (c3 12.19 -> 12.52 us)
     constexpr bool PENDING_ON_HELPER = HELP && LPE == 4;
+    __shared__ uint4 s_cpend_all[PENDING_ON_HELPER ? 1 : WPG][PENDING_ON_HELPER ? 1 : QENV];   // see c_pend
     // the planet update on the helpers: pair instance only (the quad instance
     // of c2 lost with it there: 5.08 -> 5.33 us, ab_quad_planets_on_helper.jsonl)
     constexpr bool PLANETS_ON_HELPER = HELP && LPE == 2;
@@ -2506,7 +2581,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #pragma unroll
                 for (int m = 0; m < PPL; ++m) {
                     const int j = q + LPE * m;
-                    if (j < np) planets[size_t(j) * NN + i] = hout[m];
+                    if (j < np) st_out(&planets[size_t(j) * NN + i], hout[m]);
                 }
             }
             if (PENDING_ON_HELPER && q == 0 && active && !((todo0 >> lane) & 1ull)) {   // a surviving env: its
@@ -2588,7 +2663,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const uint32_t hw = uint32_t(h.y);
     int np = hw1_np(hw);
     const int flags = hw1_flags(hw);
-    const int half = hw1_half(hw);   // the env's bullet group's half (this step writes the other)
     const int nb = active ? min(hw1_nb(hw), p.b_cap) : 0;
     np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
     if constexpr (PLANETS_AFTER_HDR) {
@@ -2617,8 +2691,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const bool live = tick < p.timeout_tick;
     const bool t0 = tick == 0;
     STAMP(1);
-    const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
-    const bool fires = ((fire_word >> (tick & 31)) & 1u) != 0;
+    const bool fires = fires_at(p, tick, live);
     uint32_t pend_key = uint32_t(h.w);
     n_pl += active && q == 0 ? uint32_t(np) : 0u;
 
@@ -2627,6 +2700,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     //      during the physics below
     const BulletsIn<T> bin = bullets_begin<T, LPE>(p, st, lane, e, q, base, nb, hw, active && fires ? S : 0, t0,
                                                    s_index, s_kept, s_hit, s_serial, s_dst);
+    // the env's bullet group's half (this step writes the other): from the
+    // wave-uniform values, not held per lane
+    auto half_of_env = [&]() { return e >= BGROUP ? bin.half1 : bin.half0; };
     const int total = bin.total;
     STAMP(19);
     // key[397] of the next game's seed (first step of a game): a random
@@ -2806,6 +2882,12 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     STAMP(3);
     // ---- bullets (core.py:241-251, 264-266, 295-300): collide with the old
     //      bodies, move, cull, compact into the other half (bullets_rounds)
+    // the stream cursor (c_pend) for the header's pending-seed check goes to
+    // LDS before the bullet pass: held in registers across it, it was
+    // spilled to scratch right after its load, with a wait for every load
+    // in flight (the pair instance with helpers at 128 VGPRs)
+    uint4 (*s_cpend)[PENDING_ON_HELPER ? 1 : QENV] = s_cpend_all;
+    if (!PENDING_ON_HELPER && q == 0) s_cpend[PENDING_ON_HELPER ? 0 : wv][PENDING_ON_HELPER ? 0 : e] = c_pend;
     bullets_rounds<T, S, PMAX, LPE>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf, s_body, s_index, s_kept,
                                     s_hit, s_dst, gp, gs STAMP_PASS);
     if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
@@ -2813,7 +2895,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     }
     const int wr_in = s_kept[e];
     const int hit_bits = s_hit[e];
-    const int dst_off = s_dst[e];   // the env's first entry in the other half
+    const int dst_off = s_dst[e];   // the env's first entry in its group's region of the other half
     // the stores below recompute their addresses from an opaque copy of the
     // env index (holding the load addresses live across the bullet pass
     // costs registers the bullet pass needs)
@@ -2873,7 +2955,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 }
                 const uint64_t nib = (__ballot(keep) >> (lane & ~(LPE - 1))) & ((1ull << LPE) - 1);
                 const int pos = wr + __popcll(nib & ((1ull << q) - 1));
-                if (keep && pos < p.b_cap) bullets[bullet_base(st, p, half ^ 1, is) + size_t(dst_off + pos)] = out;
+                if (keep && pos < p.b_cap)
+                    st_out(&bullets[bullet_groups<LPE>(st, p, base, bin.half0, bin.half1).dst_of(uint32_t(e)) +
+                                    size_t(dst_off + pos)], out);
                 wr += __popcll(nib);
             }
             const int w = wr < p.b_cap ? wr : p.b_cap;
@@ -2888,8 +2972,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 v.y = T(wrap_unit<double>(my + p.dt * ndy));
                 v.z = T(ndx);
                 v.w = T(ndy);
-                ships[size_t(q) * NN + is] = v;
-                ships_b[size_t(q) * NN + is] = T(mb + p.db * double((ctl >> 1) - 1));
+                st_out(&ships[size_t(q) * NN + is], v);
+                st_out(&ships_b[size_t(q) * NN + is], T(mb + p.db * double((ctl >> 1) - 1)));
             }
 
             STAMP(6);
@@ -2900,23 +2984,25 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #pragma unroll
                 for (int m = 0; m < PPL; ++m) {
                     const int j = q + LPE * m;
-                    if (j < np) planets[size_t(j) * NN + is] = pout[m];
+                    if (j < np) st_out(&planets[size_t(j) * NN + is], pout[m]);
                 }
             }
 
             STAMP(7);
             if (q == 0) {
                 const int fl = flags | (dropped ? 1 : 0);
-                const int w1 = hw1(np, fl, half ^ 1, w, dst_off);
+                const int w1 = hw1(np, fl, half_of_env() ^ 1, w, dst_off);
                 if constexpr (PENDING_ON_HELPER) {   // words 2-3: the helper's
-                    reinterpret_cast<int2 *>(st.hdr)[2 * is] = make_int2(tick + 1, w1);
+                    st_out(&reinterpret_cast<int2 *>(st.hdr)[2 * is], make_int2(tick + 1, w1));
                 } else {
 #ifdef ASTRO_ABLATE_PENDING
                     const uint32_t kv = key_valid ? KEY_VALID : 0u;
 #else
-                    const uint32_t kv = check_pending(p, st, is, key_valid, undrawn, c_pend, pend_seed, pend_key);
+                    const uint32_t kv = check_pending(p, st, is, key_valid, undrawn,
+                                                      s_cpend[PENDING_ON_HELPER ? 0 : wv][PENDING_ON_HELPER ? 0 : e],
+                                                      pend_seed, pend_key);
 #endif
-                    reinterpret_cast<int4 *>(st.hdr)[is] = make_int4(tick + 1, w1, int(pend_seed | kv), int(pend_key));
+                    st_out(&reinterpret_cast<int4 *>(st.hdr)[is], make_int4(tick + 1, w1, int(pend_seed | kv), int(pend_key)));
                 }
                 n_bout += uint32_t(w);
                 n_drop += uint32_t(dropped);
@@ -2929,7 +3015,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             need_reset = auto_reset && q == 0;
             f_reset = need_reset;
             if (!auto_reset && q == 0)   // no bullets, and in the group's new half (the rest is left for astro_reset)
-                reinterpret_cast<int *>(st.hdr)[4 * size_t(is) + 1] = hw1(np, flags, half ^ 1, 0, 0);
+                reinterpret_cast<int *>(st.hdr)[4 * size_t(is) + 1] = hw1(np, flags, half_of_env() ^ 1, 0, 0);
         }
     }
 
@@ -2939,7 +3025,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     if constexpr (!HELP)
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
         todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
-                                                undrawn, half ^ 1, s_chain, s_serial STAMP_PASS);
+                                                undrawn, half_of_env() ^ 1, s_chain, s_serial STAMP_PASS);
     if (!HELP && auto_reset) {
         wave_sync();
         if (stats) c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));
@@ -2948,7 +3034,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
             const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, undrawn, c,
                                                 stream_ring_of(st, is));
-            restart_env<T, S, PMAX, LPE>(p, st, is, ng, half ^ 1, q);
+            restart_env<T, S, PMAX, LPE>(p, st, is, ng, half_of_env() ^ 1, q);
         }
     }
     STAMP(10);
@@ -3015,21 +3101,25 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 // 8 planet slots: 3 (141 VGPRs, no spills; at 4: 128 VGPRs, 41 spilled, c5
 // 34.3 -> 31.1 us); 4 slots: 3 (135 VGPRs, no spills; at 4: 7 spilled, c3 at
 // 1M envs 139.6 -> 127.1 us, at 256k 39.5 -> 37.3 us, ab_p4_waves.jsonl)
-// (-DASTRO_P4_WAVES / _P8_WAVES / _MULTI_WAVES: occupancy A/B builds only)
+// The K-tick (rollout) instances: 4 planet slots at 3 waves per SIMD (168
+// VGPRs; at 2 the 1M-env rollouts ran 110 vs 91 us per tick,
+// profiles/round4/ab_packed_bullets_v1.jsonl), 8 slots and the ScriptBot
+// instance at 2 (at 3 they spill 25 / 55 VGPRs).
+// (-DASTRO_P4_WAVES / _P8_WAVES / _M4_WAVES: occupancy A/B builds only)
 #ifndef ASTRO_P8_WAVES
 #define ASTRO_P8_WAVES 3
 #endif
 #ifndef ASTRO_P4_WAVES
 #define ASTRO_P4_WAVES 3
 #endif
-#ifndef ASTRO_MULTI_WAVES
-#define ASTRO_MULTI_WAVES 2
+#ifndef ASTRO_M4_WAVES
+#define ASTRO_M4_WAVES 3
 #endif
-constexpr int P8_WAVES = ASTRO_P8_WAVES, P4_WAVES = ASTRO_P4_WAVES, MULTI_WAVES = ASTRO_MULTI_WAVES;
+constexpr int P8_WAVES = ASTRO_P8_WAVES, P4_WAVES = ASTRO_P4_WAVES, M4_WAVES = ASTRO_M4_WAVES;
 
 template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false, bool HELP = false,
           int WPG = QW>
-__global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? MULTI_WAVES : (PMAX > 4 ? P8_WAVES : P4_WAVES)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
+__global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS || PMAX > 4 ? 2 : M4_WAVES) : (PMAX > 4 ? P8_WAVES : P4_WAVES)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
                                                                 unsigned long long *stats, int auto_reset) {
@@ -3284,7 +3374,9 @@ int check_params(const AstroParams *p) {
         return fail(-14, "max_planets must be in [1, p_pad]");
     if (p->b_cap < 1 || p->b_cap > ASTRO_MAX_B_CAP) return fail(-15, "b_cap must be in [1, %d]", ASTRO_MAX_B_CAP);
     if (p->timeout_tick < 0 || p->timeout_tick >= int(TICK_MASK)) return fail(-16, "timeout_tick out of [0, 2^22)");
-    if (p->timeout_tick > 0 && !p->fire_bits) return fail(-17, "fire_bits is NULL");
+    if (p->timeout_tick > 0 && !p->fire_bits && p->fire_period <= 0) return fail(-17, "fire_bits is NULL");
+    if (p->fire_period > 0 && (p->fire_phase < 0 || p->fire_phase >= p->fire_period))
+        return fail(-17, "fire_phase must be in [0, fire_period)");
     if (p->kernel < 0 || p->kernel > 3) return fail(-18, "kernel must be 0 (auto), 1 (lane), 2 (quad) or 3 (pair)");
     if (p->planets_only < 0 || p->planets_only > p->max_planets)
         return fail(-19, "planets_only must be in [0, max_planets]");

@@ -234,10 +234,12 @@ class BatchedEnv:
 
         k = _schedule.kernel_constants(config)
         self.key_table = key_table(dev) if use_key_table else None
+        period, phase = self.schedule.fire_period()
         self.params = _lib.AstroParams(
             p_pad=self.p_pad, b_cap=self.b_cap, timeout_tick=self.schedule.timeout_tick,
             fire_bits=self.fire_bits.data_ptr(), kernel=_lib.KERNELS[kernel], planets_only=planets_only,
-            key_table=self.key_table.data_ptr() if self.key_table is not None else None, **k)
+            key_table=self.key_table.data_ptr() if self.key_table is not None else None,
+            fire_period=period, fire_phase=phase, **k)
         self.state = _lib.AstroState(
             ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),
             planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),

@@ -261,11 +261,11 @@ def stub_rank(args, world, rank):
         print(json.dumps(out), flush=True)
 
 
-PROFILE_ROUNDS = ('round3', 'round2')
+PROFILE_ROUNDS = ('round4', 'round3', 'round2')
 
 
 def profile_file(name):
-    """The newest committed profile of that name (profiles/round3, then round2)."""
+    """The newest committed profile of that name (profiles/round4, round3, then round2)."""
     for r in PROFILE_ROUNDS:
         p = os.path.join(ROOT, 'profiles', r, name)
         if os.path.exists(p):

@@ -81,6 +81,10 @@ typedef struct AstroParams {
     const uint32_t *key_table; /* device, optional: key[397] of MT19937 init_genrand for
                                   every seed < 2^30 (astro_keytable_build); NULL = the
                                   397-step chain at each create (~9 us per lane) */
+    int32_t fire_period;   /* > 0: the schedule is exactly "fire on tick k iff k % fire_period
+                              == fire_phase" for every k < timeout_tick (fire_bits may then
+                              be NULL and is not read); 0: fire_bits decides */
+    int32_t fire_phase;
 } AstroParams;
 
 /* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:

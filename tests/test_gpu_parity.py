@@ -263,7 +263,36 @@ def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap, kernel):
     """N envs with auto-reset, float32 state: every tick equals the oracle
     stepped from the kernel's own input state, resets draw the right seeds
     and create the right games, overflow (small b_cap) is counted alike."""
-    cfg = CFG[name]
+    _auto_reset_vs_oracle(CFG[name], name, n, ticks, bcap, kernel)
+
+
+@pytest.mark.parametrize('kernel', KERNELS)
+def test_fire_schedule_table_path(kernel):
+    """A config whose fire schedule is not periodic (reload_time 0.33: the
+    kernel reads the fire bitmask) against the oracle, and the default
+    config run both ways -- periodic arguments (fire_period 15, phase 14) and
+    the bitmask -- bit for bit on every array, packed bullet halves included
+    (the spawn slots a fire tick reserves place the bullets)."""
+    from astro_amd import schedule
+    cfg = CFG['default']._replace(reload_time=0.33)
+    assert schedule.build(cfg).fire_period() == (0, 0)
+    _auto_reset_vs_oracle(cfg, 'reload0.33', 600, 60, 32, kernel)
+    base = CFG['default']
+    assert schedule.build(base).fire_period() == (15, 14)
+    g = torch.Generator(device='cuda').manual_seed(11)
+    ctls = torch.randint(0, 6, (150, 2000, 2), generator=g, device='cuda', dtype=torch.int8)
+    envs = [_env(base, 2000, dtype=torch.float32, b_cap=32, auto_reset=True, kernel=kernel) for _ in range(2)]
+    envs[1].params.fire_period = 0
+    for e in envs:
+        e.reset()
+        for t in range(150):
+            e.step(ctls[t])
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream'):
+        assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), f
+    assert envs[0].stat_dict()['bullets_in'] > 0
+
+
+def _auto_reset_vs_oracle(cfg, name, n, ticks, bcap, kernel):
     P = batched.make_params(cfg)
     env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, auto_reset=True, kernel=kernel)
     env.reset()

@@ -138,6 +138,26 @@ def test_schedule_matches_oracle_and_golden():
         assert sc.t[:50].tolist() == s['t'] and sc.reload[:50].tolist() == s['reload']
 
 
+def test_fire_period_detection():
+    """The kernel's periodic fire arguments (AstroParams.fire_period/phase)
+    are set only when they reproduce the float64 schedule on every tick
+    before the timeout: the presets (default: ticks 14 + 15k; SOLO: never)
+    and reload 0.1 are periodic; reload 0.07 / 0.33 and dt 0.017 drift off
+    any period and keep the bitmask."""
+    from astro_amd.config import SOLO_EASY_CONFIG
+    cases = [(DEFAULT_CONFIG, (15, 14)), (SOLO_CONFIG, (1 << 30, (1 << 30) - 1)),
+             (SOLO_EASY_CONFIG, (1 << 30, (1 << 30) - 1)), (DEFAULT_CONFIG._replace(reload_time=0.1), (5, 4)),
+             (DEFAULT_CONFIG._replace(reload_time=0.07), (0, 0)), (DEFAULT_CONFIG._replace(reload_time=0.33), (0, 0)),
+             (DEFAULT_CONFIG._replace(dt=0.017), (0, 0))]
+    for cfg, want in cases:
+        sch = schedule.build(cfg)
+        got = sch.fire_period()
+        assert got == want, (cfg, got)
+        if got[0]:
+            k = np.arange(sch.timeout_tick)
+            assert np.array_equal((k % got[0]) == got[1], sch.fire)
+
+
 def test_kernel_constants_match_oracle():
     for cfg in gio.configs().values():
         k = schedule.kernel_constants(cfg)

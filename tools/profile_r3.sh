@@ -12,7 +12,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 WL=${WL:-c3}
-OUT=gpurun_out/r3prof/$WL
+OUT=${OUT:-gpurun_out/prof/$WL}
 mkdir -p $OUT
 ARGS="--workload $WL --no-cpu --no-single --no-features --steps ${PSTEPS:-300} ${EXTRA_ARGS:-}"
 run() {
