@@ -68,10 +68,14 @@ template <typename T> struct Store;
 template <> struct Store<float> { using V = F4; };
 template <> struct Store<double> { using V = D4; };
 
-// A state store of the step (A/B build -DASTRO_NT_STORES: nontemporal)
+// A state store of the step: nontemporal (the next launch reads it from
+// HBM anyway; streamed, the stores leave L2 to the launch's loads: c3 12.28
+// -> 12.05 us, c2 5.58 -> 5.44 us, c5 32.42 -> 32.08 us,
+// profiles/round4/ab_packed_bullets_v5v6.jsonl).  A/B build
+// -DASTRO_TEMPORAL_STORES: plain stores
 template <typename X>
 __device__ __forceinline__ void st_out(X *p, const X &v) {
-#ifdef ASTRO_NT_STORES
+#ifndef ASTRO_TEMPORAL_STORES
     if constexpr (sizeof(X) == 16 && alignof(X) == 16) {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(*reinterpret_cast<const v4u *>(&v), reinterpret_cast<v4u *>(p));
@@ -847,7 +851,17 @@ constexpr int BLOCK = 64;
 // costs no load; any other reads the fire bitmask -- a load keyed by the
 // header's tick, whose latency lands on whatever needs the answer first.
 __device__ __forceinline__ bool fires_at(const AstroParams &p, int tick, bool live) {
-    if (p.fire_period > 0) return live && uint32_t(tick) % uint32_t(p.fire_period) == uint32_t(p.fire_phase);
+    if (p.fire_period > 0) {
+        // tick mod period by a float quotient (tick < 2^22 is exact in float;
+        // the approximate reciprocal and the product's rounding leave the
+        // quotient at most one off, fixed below): a few instructions instead
+        // of an integer division
+        const int per = p.fire_period;
+        const int qt = int(float(tick) * __builtin_amdgcn_rcpf(float(per)));
+        int r = tick - qt * per;
+        r = r < 0 ? r + per : (r >= per ? r - per : r);
+        return live && r == p.fire_phase;
+    }
     const uint32_t w = p.fire_bits[(live ? tick : 0) >> 5];
     return live && ((w >> (tick & 31)) & 1u) != 0;
 }
@@ -2099,11 +2113,6 @@ __device__ __forceinline__ void report_error(const AstroState &st, uint32_t bits
 // pair kernel's 32): each group's region in the half it is read from and in
 // the half it is written to (wave-uniform; every env of a group is in the
 // same half)
-__device__ __forceinline__ size_t uniform64(size_t v) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v)), hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
-    return size_t(lo) | (size_t(hi) << 32);
-}
-
 struct BulletGroups {
     // group 0's regions and group 1's minus group 0's: a select between
     // two values (a select between two members became an indexed load from
@@ -2123,22 +2132,27 @@ struct BulletsIn {
     typename Store<T>::V cur0, cur1;
 };
 
-// the wave's bullet groups' regions (recomputed where needed: scalar work,
-// cheaper than holding eight SGPRs across the physics)
+// the wave's bullet groups' regions (recomputed where needed: a few scalar
+// instructions, cheaper than holding eight SGPRs across the physics).  Every
+// operand is made wave-uniform first, so the 64-bit products are scalar
+// multiplies (from a lane value they were 64-bit vector multiplies and eight
+// readfirstlanes in front of the bullet pass)
 template <int LPE>
 __device__ __forceinline__ BulletGroups bullet_groups(const AstroState &st, const AstroParams &p, int base, int half0,
                                                       int half1) {
+    const uint32_t bcs = uint32_t(p.b_cap + p.nships), n = uint32_t(st.n_env);
+    const uint32_t g0 = __builtin_amdgcn_readfirstlane(uint32_t(base) & ~uint32_t(BGROUP - 1));
+    const uint32_t h0 = __builtin_amdgcn_readfirstlane(uint32_t(half0));
+    auto at = [&](uint32_t h, uint32_t g) { return size_t(h ? n + g : g) * size_t(bcs); };   // bullet_base
     BulletGroups g;
-    const size_t src0 = bullet_base(st, p, half0, base), dst0 = bullet_base(st, p, half0 ^ 1, base);
-    size_t dsrc = 0, ddst = 0;
+    g.src0 = at(h0, g0);
+    g.dst0 = at(h0 ^ 1u, g0);
+    g.dsrc = g.ddst = 0;
     if constexpr (64 / LPE > BGROUP) {   // (pair: the wave's second bullet group starts at env 16)
-        dsrc = bullet_base(st, p, half1, base + BGROUP) - src0;
-        ddst = bullet_base(st, p, half1 ^ 1, base + BGROUP) - dst0;
+        const uint32_t h1 = __builtin_amdgcn_readfirstlane(uint32_t(half1));
+        g.dsrc = at(h1, g0 + BGROUP) - g.src0;
+        g.ddst = at(h1 ^ 1u, g0 + BGROUP) - g.dst0;
     }
-    g.src0 = uniform64(src0);   // (wave-uniform: in SGPRs)
-    g.dsrc = uniform64(dsrc);
-    g.dst0 = uniform64(dst0);
-    g.ddst = uniform64(ddst);
     return g;
 }
 
@@ -2150,10 +2164,27 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroParams &p, cons
     using V = typename Store<T>::V;
     const V *bullets = reinterpret_cast<const V *>(st.bullets);
     BulletsIn<T> b;
+    if (__builtin_amdgcn_readfirstlane(__any((nb | res) != 0)) == 0) {   // uniform: no live bullet and no
+        b.total = 0;                                                     // spawn in the wave (config 2)
+        b.off = 0;
+        b.half0 = b.half1 = __builtin_amdgcn_readfirstlane(hw1_half(hw));
+        b.tag = b.bw0 = b.bw1 = 0u;
+        b.cur0 = b.cur1 = V{};
+        if (q == 0) {
+            s_kept[e] = 0;
+            s_hit[e] = 0;
+            s_serial[e] = 0;
+            s_dst[e] = 0;
+        }
+        return b;
+    }
     // one scan for both: the wave's live bullets (low half: their dense
     // numbering) and, per bullet group, live bullets + the S spawn slots of
     // the envs that fire this tick (high half: where each env's bullets go
-    // in the other half); a wave's sums are < 2^16 (nb <= b_cap <= 1000)
+    // in the other half); a wave's sums are < 2^16 (nb <= b_cap <= 1000).
+    // (Reserving S slots for every env instead keeps the fire test off the
+    // scan, but the holes it leaves spread a group's reads over ~50% more
+    // lines: c3 12.07 -> 12.54 us, profiles/round4/ab_packed_bullets_v8v9.jsonl)
     const int v = q == 0 ? nb | ((nb + res) << 16) : 0;
     const int incl = wave_incl_scan(v, lane);
     b.off = (incl & 0xffff) - nb;
@@ -2195,7 +2226,7 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroParams &p, cons
 // sxf/syf: both ships' old positions (float32); mpxf/mpyf: the lane's own
 // planet slots q + LPE m (float32, slots past the env's planets parked at
 // -FAR_POS).  Ends with the wave's LDS results readable (wave_sync).
-template <typename T, int S, int PMAX, int LPE>
+template <typename T, int S, int PMAX, int LPE, int NRW = 2>
 __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const AstroState &st, const BulletsIn<T> &b,
                                                int lane, int e, int q, int base, int nb, const float (&sxf)[S],
                                                const float (&syf)[S], const float (&mpxf)[PMAX / LPE],
@@ -2393,9 +2424,12 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           uint32_t bws[3] = {bw0, bw1, 0u};
           V curs[3] = {cur0, cur1, cur0};
           const int nr = (wend - w0 + 63) / 64;   // uniform
-          // two rounds side by side with 4 planet slots; with 8 the registers
-          // of two rounds spill (measured: c5 30.8 -> 34.3 us), one at a time
-          constexpr int NR2 = PMAX <= 4 ? 2 : 1;
+          // two rounds side by side with 4 planet slots (NRW = 2: the launches
+          // latency sets, with helper waves or K ticks); with 8 the registers
+          // of two rounds spill (measured: c5 30.8 -> 34.3 us), and the
+          // one-tick instances without helpers (millions of envs, HBM-bound)
+          // keep the registers for occupancy instead: one at a time
+          constexpr int NR2 = PMAX <= 4 ? NRW : 1;
           if (nr >= 3) {
               bws[2] = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
               curs[2] = bullets[g.src_of(bws[2])];
@@ -2443,7 +2477,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // step waves are the critical path (c2 5.36 -> 5.20 us A/B); in the pair
     // instance the helpers' resets are the tail (c3 12.19 -> 12.52 us)
     constexpr bool PENDING_ON_HELPER = HELP && LPE == 4;
-    __shared__ uint4 s_cpend_all[PENDING_ON_HELPER ? 1 : WPG][PENDING_ON_HELPER ? 1 : QENV];   // see c_pend
+    __shared__ uint4 s_cpend_all[HELP && !PENDING_ON_HELPER ? WPG : 1][HELP && !PENDING_ON_HELPER ? QENV : 1];   // see c_pend
     // the planet update on the helpers: pair instance only (the quad instance
     // of c2 lost with it there: 5.08 -> 5.33 us, ab_quad_planets_on_helper.jsonl)
     constexpr bool PLANETS_ON_HELPER = HELP && LPE == 2;
@@ -2491,10 +2525,23 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             // its end: it waits for this word, so the header read here is the
             // launch's input whatever the memory system's timing (the store
             // depends on the loaded value: it waits for the load's return)
-            if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
             const uint32_t hseed = uint32_t(hh.z) & SEED_MASK;
             const bool kvalid = (uint32_t(hh.z) & KEY_VALID) != 0;
             const bool hud = (uint32_t(hh.z) & UNDRAWN) != 0;   // (a reset then takes the serial path)
+            if constexpr (!PENDING_ON_HELPER) {
+                // the stream cursor the step wave's pending-seed check
+                // (check_pending, at its end) needs, into LDS: the step wave
+                // does not hold it in registers across its bullet pass (it
+                // spilled) nor waits for it anywhere; `seen` (below) orders it
+                // before the step wave's read
+                const bool want_c = q == 0 && (hud || (!kvalid && p.key_table && p.planets_only));
+                uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
+                asm volatile("" : "+s"(c_stream), "+s"(c_hdr));
+                const uint4 c = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
+                if (q == 0) s_cpend_all[wv][e] = c;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the cursor before the flag)
+            }
+            if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
             uint32_t hkey = uint32_t(hh.w);
             const bool hk = kvalid || p.key_table != nullptr;
             if (q == 1 && !kvalid && !hud) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
@@ -2723,9 +2770,11 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #else
     const bool want_c = !PENDING_ON_HELPER && q == 0 && (undrawn || (!key_valid && p.key_table && p.planets_only));
 #endif
+    // (with helper waves, the helper loads it into LDS: s_cpend)
     uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
     asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // values, not a select between the fields' addresses
-    const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
+    uint4 c_pend = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (!HELP) c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
 
     // ---- quad broadcasts: all planets, both ships
     double px[PMAX], py[PMAX], sx[S], sy[S];
@@ -2882,13 +2931,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     STAMP(3);
     // ---- bullets (core.py:241-251, 264-266, 295-300): collide with the old
     //      bodies, move, cull, compact into the other half (bullets_rounds)
-    // the stream cursor (c_pend) for the header's pending-seed check goes to
-    // LDS before the bullet pass: held in registers across it, it was
-    // spilled to scratch right after its load, with a wait for every load
-    // in flight (the pair instance with helpers at 128 VGPRs)
-    uint4 (*s_cpend)[PENDING_ON_HELPER ? 1 : QENV] = s_cpend_all;
-    if (!PENDING_ON_HELPER && q == 0) s_cpend[PENDING_ON_HELPER ? 0 : wv][PENDING_ON_HELPER ? 0 : e] = c_pend;
-    bullets_rounds<T, S, PMAX, LPE>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf, s_body, s_index, s_kept,
+    bullets_rounds<T, S, PMAX, LPE, (HELP || OPAQUE) ? 2 : 1>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf, s_body, s_index, s_kept,
                                     s_hit, s_dst, gp, gs STAMP_PASS);
     if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
         if (!wait_lds_word(s_box_all[wv].seen)) report_error(st, ASTRO_ERR_HEADER_WAIT, lane);
@@ -2998,8 +3041,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #ifdef ASTRO_ABLATE_PENDING
                     const uint32_t kv = key_valid ? KEY_VALID : 0u;
 #else
+                    // (the stream cursor: its helper's copy in LDS, see s_cpend)
                     const uint32_t kv = check_pending(p, st, is, key_valid, undrawn,
-                                                      s_cpend[PENDING_ON_HELPER ? 0 : wv][PENDING_ON_HELPER ? 0 : e],
+                                                      HELP ? s_cpend_all[HELP ? wv : 0][HELP ? e : 0] : c_pend,
                                                       pend_seed, pend_key);
 #endif
                     st_out(&reinterpret_cast<int4 *>(st.hdr)[is], make_int4(tick + 1, w1, int(pend_seed | kv), int(pend_key)));

@@ -158,6 +158,21 @@ def test_fire_period_detection():
             assert np.array_equal((k % got[0]) == got[1], sch.fire)
 
 
+def test_fire_period_float_quotient():
+    """fires_at's tick mod period (astro_kernels.hip) by a float32 quotient and
+    one correction step equals the integer remainder for every tick below
+    2^22 the kernel allows, for small, preset and huge periods (numpy float32
+    is the device's IEEE arithmetic: correctly rounded 1/period, product,
+    truncation)."""
+    ticks = np.arange(1 << 22, dtype=np.int64)
+    for per in (1, 2, 3, 5, 7, 15, 16, 97, 1000, 4095, (1 << 22) - 3, (1 << 22) + 5, 1 << 30):
+        inv = np.float32(1.0) / np.float32(per)
+        qt = (ticks.astype(np.float32) * inv).astype(np.int64)
+        r = ticks - qt * per
+        r = np.where(r < 0, r + per, np.where(r >= per, r - per, r))
+        assert np.array_equal(r, ticks % per), per
+
+
 def test_kernel_constants_match_oracle():
     for cfg in gio.configs().values():
         k = schedule.kernel_constants(cfg)
