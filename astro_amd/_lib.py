@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # (ASTRO_LIB: another build of the same library, e.g. an A/B variant from tools/build_var.sh)
 LIB_PATH = os.environ.get('ASTRO_LIB') or os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
@@ -49,8 +49,6 @@ class AstroParams(ctypes.Structure):
         ('kernel', ctypes.c_int32),
         ('planets_only', ctypes.c_int32),
         ('key_table', ctypes.c_void_p),
-        ('fire_period', ctypes.c_int32),
-        ('fire_phase', ctypes.c_int32),
     ]
 
 

@@ -23,7 +23,7 @@ import torch
 from . import _lib
 from .config import (Bodies, Config, DEFAULT_CONFIG, Game, SOLO_CONFIG,  # noqa: F401
                      SOLO_EASY_CONFIG, State, Tick, generate_configs, nships)
-from .env import MAX_B_CAP, BatchedEnv, hdr_word1
+from .env import BatchedEnv
 
 _ENVS = {}
 
@@ -110,13 +110,9 @@ class _Shim:
         self.lock = threading.Lock()
         S, P = env.S, env.p_pad
         f8, i4 = np.float64, np.int32
-        # bullets: the one env's bullet group, two halves (include/astro_step.h);
-        # a tick's input is written to half 0 from entry 0, the kernel writes
-        # the output to half 1 from entry 0
         self.arena = a = _Arena(env.lib, (
             ('hdr', (1, 4), i4), ('ships', (S, 1, 4), f8), ('ships_b', (S, 1), f8), ('planets', (P, 1, 4), f8),
-            ('bullets', (2, b_cap + S, 4), f8), ('control', (1, S), np.int8), ('fire', (2,), i4),
-            ('seed', (1,), np.uint32),
+            ('bullets', (1, b_cap, 4), f8), ('control', (1, S), np.int8), ('fire', (2,), i4), ('seed', (1,), np.uint32),
             ('reward', (1, S), np.float32), ('done', (1,), np.uint8), ('errors', (1,), np.uint32)),
             env.device, mode or SHIM_MODE)
         self.in_bytes = a.end('seed')   # hdr .. seed: a tick's input
@@ -136,7 +132,6 @@ class _Shim:
                 p = type(env.params).from_buffer_copy(env.params)
                 p.timeout_tick = tick if to else tick + 1
                 p.fire_bits = a.ptr('fire')
-                p.fire_period = 0   # (this call's fire word decides, not the config's periodic schedule)
                 self.params[tick, to] = p
 
     def stream(self):
@@ -163,23 +158,14 @@ class _Shim:
                                             self.arena.ptr('seed'), None, self.stream()), 'astro_reset')
         self.sync()
 
-    def bullets_out(self):
-        """The game's live bullets (rows) where the header says they are."""
-        w1 = int(self.h['hdr'].view(np.uint32)[0, 1])
-        nb, half, boff = (w1 >> 8) & 0x3ff, (w1 >> 7) & 1, w1 >> 18
-        return self.h['bullets'][half, boff:boff + nb]
-
     def state_of(self):
         """Reference-shaped State from the mapped arrays."""
         h = self.h
         hdr = h['hdr'].view(np.uint32)
-        bl = self.bullets_out()
-        rows = np.zeros((1, self.env.b_cap, 4))
-        rows[0, :bl.shape[0]] = bl
         host = dict(ships=h['ships'].transpose(1, 0, 2), ships_b=h['ships_b'].transpose(1, 0),
-                    planets=h['planets'].transpose(1, 0, 2), bullets=rows,
-                    tick=hdr[:, 0] & 0x3fffff, nplanets=hdr[:, 1] & 0x1f, nbullets=np.array([bl.shape[0]]),
-                    flags=(hdr[:, 1] >> 5) & 3)
+                    planets=h['planets'].transpose(1, 0, 2), bullets=h['bullets'],
+                    tick=hdr[:, 0] & 0x3fffff, nplanets=hdr[:, 1] & 0xff, nbullets=(hdr[:, 1] >> 16) & 0xffff,
+                    flags=(hdr[:, 1] >> 8) & 0xff)
         return self.env.state_of(0, host)
 
 
@@ -187,13 +173,10 @@ def _shim(config, bullets_needed):
     key = (config._replace(seed=0), _device())
     sh = _ENVS.get(key)
     if sh is None or sh.env.b_cap < bullets_needed:
-        if bullets_needed > MAX_B_CAP:
-            raise ValueError('a state with %d bullets: the kernel holds at most %d per game'
-                             % (bullets_needed, MAX_B_CAP))
         cap = 64 if sh is None else sh.env.b_cap
         while cap < bullets_needed:
             cap *= 2
-        sh = _Shim(config, min(cap, MAX_B_CAP), key[1])
+        sh = _Shim(config, cap, key[1])
         _ENVS[key] = sh
     return sh
 
@@ -237,14 +220,14 @@ def _step(sh, state, control, config, S, nb):
     # the input, written straight into the memory the kernel reads
     hdr = h['hdr'].view(np.uint32)
     hdr[0, 0] = (int(hdr[0, 0]) & ~0x3fffff & 0xffffffff) | tick
-    hdr[0, 1] = hdr_word1(npl, 0, 0, nb, 0)
+    hdr[0, 1] = npl | (nb << 16)
     sx = h['ships']
     sx[:, 0, 0:2] = state.ships.x
     sx[:, 0, 2:4] = state.ships.dx
     h['ships_b'][:, 0] = state.ships.b
     h['planets'][:npl, 0, 0:2] = state.planets.x
     h['planets'][:npl, 0, 2:4] = state.planets.dx
-    if nb:   # half 0, from entry 0
+    if nb:
         h['bullets'][0, :nb, 0:2] = state.bullets.x
         h['bullets'][0, :nb, 2:4] = state.bullets.dx
     h['control'][0] = control
@@ -269,7 +252,8 @@ def _step(sh, state, control, config, S, nb):
         reload -= config.reload_time
     bdt = np.float32 if fresh else np.float64
     pdt = np.float32 if npl == 1 else np.float64
-    sv, pl, bl = h['ships'][:, 0], h['planets'][:npl, 0], sh.bullets_out()
+    nb2 = int(hdr[0, 1]) >> 16
+    sv, pl, bl = h['ships'][:, 0], h['planets'][:npl, 0], h['bullets'][0, :nb2]
     new = State(
         ships=Bodies(x=sv[:, 0:2].copy(), dx=sv[:, 2:4].copy(), b=h['ships_b'][:, 0].copy()),
         planets=Bodies(x=pl[:, 0:2].astype(pdt), dx=pl[:, 2:4].astype(pdt), b=None),

@@ -68,11 +68,11 @@ template <typename T> struct Store;
 template <> struct Store<float> { using V = F4; };
 template <> struct Store<double> { using V = D4; };
 
+
 // A state store of the step: nontemporal (the next launch reads it from
-// HBM anyway; streamed, the stores leave L2 to the launch's loads: c3 12.28
-// -> 12.05 us, c2 5.58 -> 5.44 us, c5 32.42 -> 32.08 us,
-// profiles/round4/ab_packed_bullets_v5v6.jsonl).  A/B build
-// -DASTRO_TEMPORAL_STORES: plain stores
+// HBM anyway; streamed, the stores leave L2 to the launch's loads; A/B in
+// profiles/round4/ab_nt_stores.jsonl).  A/B build -DASTRO_TEMPORAL_STORES:
+// plain stores
 template <typename X>
 __device__ __forceinline__ void st_out(X *p, const X &v) {
 #ifndef ASTRO_TEMPORAL_STORES
@@ -361,34 +361,6 @@ constexpr uint32_t MT_PROLOGUE = 397;
 // key) by whoever checks the pending seed -- the step wave, or its helper
 constexpr int TICK_BITS = 22;
 constexpr uint32_t TICK_MASK = (1u << TICK_BITS) - 1;
-
-// hdr word 1 (include/astro_step.h): nplanets | flags << 5 | half << 7 |
-// nbullets << 8 | boff << 18 -- the env's live bullets are entries [boff,
-// boff + nbullets) of its bullet group's region in half `half` (see
-// bullet_base)
-__device__ __forceinline__ int hw1_np(uint32_t w) { return int(w & 31u); }
-__device__ __forceinline__ int hw1_flags(uint32_t w) { return int((w >> 5) & 3u); }
-__device__ __forceinline__ int hw1_half(uint32_t w) { return int((w >> 7) & 1u); }
-__device__ __forceinline__ int hw1_nb(uint32_t w) { return int((w >> 8) & 1023u); }
-__device__ __forceinline__ int hw1_boff(uint32_t w) { return int(w >> 18); }
-__device__ __forceinline__ int hw1(int np, int flags, int half, int nb, int boff) {
-    return int(uint32_t(np) | (uint32_t(flags) << 5) | (uint32_t(half) << 7) | (uint32_t(nb) << 8) |
-               (uint32_t(boff) << 18));
-}
-
-// Packed bullets (include/astro_step.h): two halves of n_env * (b_cap + S)
-// entries; the envs 16g .. 16g + 15 (a bullet group) keep their live bullets
-// in the group's region, entries [16g (b_cap + S), (16g + 16)(b_cap + S)) of
-// the half, env after env.  A step reads the group from one half and writes
-// it to the other: an env's new bullets start at the sum over the group's
-// earlier envs of (live bullets + the S slots a fire tick may spawn), known
-// from the headers before the bullet pass, so survivors are stored as they
-// are decided (a bullet that dies leaves a hole until the next step).
-constexpr int BGROUP = ASTRO_BULLET_GROUP;
-__device__ __forceinline__ size_t bullet_base(const AstroState &st, const AstroParams &p, int half, int i) {
-    const size_t BCS = size_t(p.b_cap + p.nships);
-    return size_t(half) * size_t(st.n_env) * BCS + size_t(i & ~(BGROUP - 1)) * BCS;
-}
 constexpr uint32_t KEY_VALID = 1u << 31;
 constexpr uint32_t UNDRAWN = 1u << 30;
 constexpr uint32_t SEED_MASK = (1u << 30) - 1;   // generate_configs seeds are randint(1 << 30)
@@ -759,17 +731,16 @@ __device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t 
 }
 
 // Start env i's next game from its NextGame: create (the float half), then
-// the stream record and header (part 0).  `half`: the bullet half the env's
-// group is in after this call (no bullets: the game is new).
+// the stream record and header (part 0).
 template <typename T, int S, int PMAX, int NPART = 1>
 __device__ __forceinline__ void restart_env(const AstroParams &p, const AstroState &st, int i,
-                                            const NextGame<S> &ng, int half, int part = 0) {
+                                            const NextGame<S> &ng, int part = 0) {
     int cf = 0;
     const int n = create_env<T, S, PMAX, NPART>(p, st, i, create_draws<S>(ng.words), cf, part);
     if (part != 0) return;
     reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(ng.ca, ng.cb, ng.ci, ng.seed);
     const int flags = (ng.exhausted || cf) ? 2 : 0;
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, hw1(n, flags, half, 0, 0), int(UNDRAWN), 0);
+    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(UNDRAWN), 0);
 }
 
 // The pending seed at the end of a step (the lane holding the env's header):
@@ -797,16 +768,6 @@ __device__ __forceinline__ uint32_t check_pending(const AstroParams &p, const As
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-// Inclusive prefix sum within each 16-lane row (DPP row shifts; a lane
-// shifted in from outside the row adds 0).  All lanes must be active.
-__device__ __forceinline__ int row_incl_scan(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
     return v;
 }
 
@@ -844,27 +805,6 @@ constexpr int NSTAMP = 24;   // 0-13 step sections, 14-15 placement, 16-19 reset
 #endif
 
 constexpr int BLOCK = 64;
-
-// Does a game fire on this tick (core.py:262-280, the host's replay of the
-// float64 reload recurrence)?  A schedule that is exactly periodic (every
-// preset: the default fires on ticks 14 + 15k) is two kernel arguments and
-// costs no load; any other reads the fire bitmask -- a load keyed by the
-// header's tick, whose latency lands on whatever needs the answer first.
-__device__ __forceinline__ bool fires_at(const AstroParams &p, int tick, bool live) {
-    if (p.fire_period > 0) {
-        // tick mod period by a float quotient (tick < 2^22 is exact in float;
-        // the approximate reciprocal and the product's rounding leave the
-        // quotient at most one off, fixed below): a few instructions instead
-        // of an integer division
-        const int per = p.fire_period;
-        const int qt = int(float(tick) * __builtin_amdgcn_rcpf(float(per)));
-        int r = tick - qt * per;
-        r = r < 0 ? r + per : (r >= per ? r - per : r);
-        return live && r == p.fire_phase;
-    }
-    const uint32_t w = p.fire_bits[(live ? tick : 0) >> 5];
-    return live && ((w >> (tick & 31)) & 1u) != 0;
-}
 
 // Where a launch's controls come from and how many ticks it runs
 // (astro_step: one tick of a control array; astro_rollout: K ticks of a
@@ -1010,12 +950,11 @@ constexpr int BCHUNK = 8;  // bullets loaded per batch: 8 loads in flight per la
 // every live bullet with the OLD planets and ships (core.py:241-251), drop the
 // hit ones (core.py:264-266), move the rest without gravity and cull those
 // with BOTH coordinates outside [-1, 1] (core.py:295-300, 195), compacting in
-// order from the env's bullets in one half (src) to its slots in the other
-// (dst).
+// order, in place (slot written <= slot read).
 template <typename C, typename T, int S, int PMAX>
-__device__ __forceinline__ void bullet_pass(const AstroParams &p, const typename Store<T>::V *src,
-                                            typename Store<T>::V *dst, int nb, int np, const double (&px)[PMAX],
-                                            const double (&py)[PMAX], const double (&sx)[S], const double (&sy)[S],
+__device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store<T>::V *bullets, size_t BC, int i,
+                                            int nb, int np, const double (&px)[PMAX], const double (&py)[PMAX],
+                                            const double (&sx)[S], const double (&sy)[S],
                                             typename Store<T>::V (&cur)[BCHUNK], bool (&hit)[S], int &w,
                                             int &dropped, bool t0) {
     using V = typename Store<T>::V;
@@ -1033,13 +972,14 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, const typename
         syf[s] = float(sy[s]);
     }
     for (int base = 0; base < nb; base += BCHUNK) {
-        // prefetch the next chunk before working on this one
+        // prefetch the next chunk before working on this one (slots read
+        // ahead are never below the write cursor: w <= slot being read)
         V nxt[BCHUNK];
         if (base + BCHUNK < nb) {
 #pragma unroll
             for (int u = 0; u < BCHUNK; ++u) {
                 const int k = base + BCHUNK + u < nb ? base + BCHUNK + u : 0;
-                nxt[u] = src[k];
+                nxt[u] = bullets[size_t(i) * BC + k];
             }
         }
 #pragma unroll
@@ -1084,7 +1024,7 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, const typename
                 v.y = T(ny);
                 v.z = T(ndx);
                 v.w = T(ndy);
-                dst[w] = v;
+                bullets[size_t(i) * BC + w] = v;
             }
             // counters as arithmetic: a conditional ++ of one of two locals
             // is folded into a store through a selected pointer, which sends
@@ -1099,8 +1039,9 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, const typename
 
 // New bullet of one ship (core.py:267-279) moved and culled like the others.
 template <typename C, typename T>
-__device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V *dst, double sx, double sy,
-                                      double sdx, double sdy, float ds, float dc, int &w, int &dropped) {
+__device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V *bullets, size_t BC, int i,
+                                      double sx, double sy, double sdx, double sdy, float ds, float dc, int &w,
+                                      int &dropped) {
     using V = typename Store<T>::V;
     const float os = p.spawn_off * ds, oc = p.spawn_off * dc;
     const float vs = p.bullet_speed * ds, vc = p.bullet_speed * dc;
@@ -1116,7 +1057,7 @@ __device__ __forceinline__ void spawn(const AstroParams &p, typename Store<T>::V
         v.y = T(ny);
         v.z = T(bdx);
         v.w = T(bdy);
-        dst[w] = v;
+        bullets[size_t(i) * BC + w] = v;
     }
     w += int(keep && fits);
     dropped += int(keep && !fits);
@@ -1130,8 +1071,13 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                                                            int auto_reset) {
     using V = typename Store<T>::V;
     const int N = st.n_env;
+#ifdef ASTRO_ENVS_PER_WAVE   // occupancy experiment: fewer envs per wave
+    const int i = blockIdx.x * ASTRO_ENVS_PER_WAVE + int(threadIdx.x);
+    const bool active = i < N && int(threadIdx.x) < ASTRO_ENVS_PER_WAVE;
+#else
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool active = i < N;
+#endif
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
     bool f_reset = false, f_coll = false, f_tout = false;
 #ifdef ASTRO_STAMPS
@@ -1139,28 +1085,16 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 #endif
     STAMP(0);
 
-    // ---- header (every lane: a 16-lane row is a bullet group); where the
-    //      env's bullets go this step: after the group's earlier envs' live
-    //      bullets and fire-tick spawn slots (a DPP scan over the row)
-    const int4 h = reinterpret_cast<const int4 *>(st.hdr)[active ? i : N - 1];
-    const uint32_t hw = uint32_t(h.y);
-    const int half = hw1_half(hw);
-    const int tick = int(uint32_t(h.x) & TICK_MASK);
-    const bool live = tick < p.timeout_tick;
-    const bool fires = fires_at(p, tick, live);
-    const int nb = active ? min(hw1_nb(hw), p.b_cap) : 0;
-    const int dst_off = row_incl_scan(nb + (active && fires ? S : 0)) - (nb + (active && fires ? S : 0));
-
     if (active) {
         const size_t NN = size_t(N);
+        const size_t BC = size_t(p.b_cap);   // bullets: [N][b_cap] rows
         V *ships = reinterpret_cast<V *>(st.ships);
         T *ships_b = reinterpret_cast<T *>(st.ships_b);
         V *planets = reinterpret_cast<V *>(st.planets);
         V *bullets = reinterpret_cast<V *>(st.bullets);
-        const V *bsrc = bullets + bullet_base(st, p, half, i) + hw1_boff(hw);
-        V *bdst = bullets + bullet_base(st, p, half ^ 1, i) + dst_off;
 
-        // ---- round 1 of loads: ships, control (independent)
+        // ---- round 1 of loads: header, ships, control (independent)
+        const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
         double sx[S], sy[S], sdx[S], sdy[S], sb[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -1180,12 +1114,15 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 #pragma unroll
             for (int s = 0; s < S; ++s) ctl[s] = tick_control<S>(drv, i, s, NN, 0);
         }
+        const int tick = int(uint32_t(h.x) & TICK_MASK);
         const bool key_valid = (uint32_t(h.z) & KEY_VALID) != 0;
         const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
         uint32_t pend_seed = uint32_t(h.z) & SEED_MASK;
-        int np = hw1_np(hw);
-        int flags = hw1_flags(hw);
+        int np = h.y & 0xff;
+        int flags = (h.y >> 8) & 0xff;
+        const int nb = int(uint32_t(h.y) >> 16);
         np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+        const bool live = tick < p.timeout_tick;
         const bool t0 = tick == 0;
         STAMP(1);
 
@@ -1202,6 +1139,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             pdx[j] = double(v.z);
             pdy[j] = double(v.w);
         }
+        const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
         // key[397] of the next game's seed, fetched once per game, off the reset path
         uint32_t pend_key = uint32_t(h.w);
         if (!key_valid && !undrawn && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
@@ -1214,7 +1152,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 #pragma unroll
         for (int u = 0; u < BCHUNK; ++u) {
             const int k = u < nb ? u : 0;
-            buf[u] = bsrc[k];
+            buf[u] = bullets[size_t(i) * BC + k];
         }
         n_pl = uint32_t(np);
         if (drv.policy == ASTRO_POLICY_BOTS) {   // ScriptBot ships decide on the old state
@@ -1289,9 +1227,9 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
         // ---- bullets
         int w = 0, dropped = 0;
         if (t0)
-            bullet_pass<float, T, S, PMAX>(p, bsrc, bdst, nb, np, px, py, sx, sy, buf, hit, w, dropped, true);
+            bullet_pass<float, T, S, PMAX>(p, bullets, BC, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, true);
         else
-            bullet_pass<double, T, S, PMAX>(p, bsrc, bdst, nb, np, px, py, sx, sy, buf, hit, w, dropped, false);
+            bullet_pass<double, T, S, PMAX>(p, bullets, BC, i, nb, np, px, py, sx, sy, buf, hit, w, dropped, false);
         n_bin = uint32_t(nb);
         STAMP(4);
 
@@ -1314,13 +1252,13 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 
         if (!done) {
             // ---- fire from the OLD ship state, after the survivors (core.py:267-280)
-            if (fires) {
+            if ((fire_word >> (tick & 31)) & 1u) {
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     if (t0)
-                        spawn<float, T>(p, bdst, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
+                        spawn<float, T>(p, bullets, BC, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
                     else
-                        spawn<double, T>(p, bdst, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
+                        spawn<double, T>(p, bullets, BC, i, sx[s], sy[s], sdx[s], sdy[s], ds[s], dc[s], w, dropped);
                 }
             }
 
@@ -1391,7 +1329,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             if (dropped) flags |= 1;
             const uint32_t kv = check_pending(p, st, i, key_valid, undrawn, c_pend, pend_seed, pend_key);
             reinterpret_cast<int4 *>(st.hdr)[i] =
-                make_int4(tick + 1, hw1(np, flags, half ^ 1, w, dst_off), int(pend_seed | kv), int(pend_key));
+                make_int4(tick + 1, np | (flags << 8) | (w << 16), int(pend_seed | kv), int(pend_key));
             n_bout = uint32_t(w);
             n_drop = uint32_t(dropped);
             STAMP(8);
@@ -1403,10 +1341,8 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                 const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
                 const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, undrawn, c,
                                                     stream_ring_of(st, i));
-                restart_env<T, S, PMAX>(p, st, i, ng, half ^ 1);
+                restart_env<T, S, PMAX>(p, st, i, ng);
                 f_reset = true;
-            } else {   // no bullets, and in the group's new half (the state is otherwise left for astro_reset)
-                reinterpret_cast<int *>(st.hdr)[4 * size_t(i) + 1] = hw1(np, flags, half ^ 1, 0, 0);
             }
             STAMP(10);
         }
@@ -1597,7 +1533,10 @@ constexpr int QWIN = 1024;        // live bullets per window of the quad kernel'
 // Inclusive prefix sum over the 64 lanes of a wave (all lanes active): DPP
 // row shifts inside each row of 16, then the row totals.
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-    v = row_incl_scan(v);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
     const int r0 = __builtin_amdgcn_readlane(v, 15);
     const int r1 = __builtin_amdgcn_readlane(v, 31);
     const int r2 = __builtin_amdgcn_readlane(v, 47);
@@ -1605,33 +1544,30 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
     return v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
 }
 
-// Bullet index word (LDS): env in the wave | slot << 5 | last-of-env << 15 |
-// position in the env's bullet-group region << 16 | tick-0 << 30 | the
-// group's half << 31 (slot < b_cap <= 1000, position < 16 (b_cap + 2))
+// Bullet index word (LDS): env in the wave | slot << 5 | last-of-env << 21 |
+// nplanets << 22 | tick-0 << 27
 __device__ __forceinline__ int bw_env(uint32_t w) { return int(w & 31u); }
-__device__ __forceinline__ int bw_slot(uint32_t w) { return int((w >> 5) & 1023u); }
-__device__ __forceinline__ bool bw_last(uint32_t w) { return (w >> 15) & 1u; }
-__device__ __forceinline__ int bw_pos(uint32_t w) { return int((w >> 16) & 16383u); }
-__device__ __forceinline__ bool bw_t0(uint32_t w) { return (w >> 30) & 1u; }
-__device__ __forceinline__ int bw_half(uint32_t w) { return int(w >> 31); }
-constexpr uint32_t BW_NEXT = (1u << 5) | (1u << 16);   // the word of the env's next slot
-__device__ __forceinline__ uint32_t bw_tag(int e, int boff, bool t0, int half) {
-    return uint32_t(e) | (uint32_t(boff) << 16) | (t0 ? 1u << 30 : 0u) | (uint32_t(half) << 31);
+__device__ __forceinline__ int bw_slot(uint32_t w) { return int((w >> 5) & 0xffffu); }
+__device__ __forceinline__ bool bw_last(uint32_t w) { return (w >> 21) & 1u; }
+__device__ __forceinline__ int bw_np(uint32_t w) { return int((w >> 22) & 31u); }
+__device__ __forceinline__ bool bw_t0(uint32_t w) { return (w >> 27) & 1u; }
+__device__ __forceinline__ uint32_t bw_tag(int e, int np, bool t0) {
+    return uint32_t(e) | (uint32_t(np) << 22) | (t0 ? 1u << 27 : 0u);
 }
 
 // Index window [w0, w0 + QWIN) of the wave's live bullets: the group of an
 // env whose bullets are numbered off .. off + nb - 1 writes the words of
 // those in the window, lane q a contiguous run of ceil(nb / LPE) slots (the
-// word of slot k + 1 is the word of slot k plus BW_NEXT: an add and an LDS
+// word of slot k + 1 is the word of slot k plus 1 << 5: an add and an LDS
 // store per slot; the last slot's flag is OR-ed in after the loop).
 template <int LPE>
 __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off, int nb, int q, uint32_t tag) {
     const int h = (nb + LPE - 1) / LPE;
     const int k0 = max(q * h, w0 - off), k1 = min(min(nb, (q + 1) * h), w0 + QWIN - off);
-    uint32_t w = tag + uint32_t(k0) * BW_NEXT;
+    uint32_t w = tag | (uint32_t(k0) << 5);
     uint32_t *dst = s_index + (off + k0 - w0);
-    for (int k = k0; k < k1; ++k, w += BW_NEXT) *dst++ = w;
-    if (k1 == nb && k1 > k0) dst[-1] = w - BW_NEXT + (1u << 15);   // last of the env
+    for (int k = k0; k < k1; ++k, w += 1u << 5) *dst++ = w;
+    if (k1 == nb && k1 > k0) dst[-1] = w - (1u << 5) + (1u << 21);   // last of the env
 }
 
 // create()'s ship s (second: s == 1 of two) and planet values from the
@@ -1738,8 +1674,7 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
 template <typename T, int S, int PMAX, int LPE, bool PRE = false>
 __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
                                                     int lane, int i, uint32_t pend_seed, uint32_t pend_key,
-                                                    bool have_key, bool undrawn, int nhalf,
-                                                    uint32_t (*s_chain)[2][13 + 2 * S],
+                                                    bool have_key, bool undrawn, uint32_t (*s_chain)[2][13 + 2 * S],
                                                     int *s_serial STAMP_ARG,
                                                     const uint32_t (*pre)[2][13 + 2 * S] = nullptr) {
     constexpr int NW = 12 + 2 * S;   // outputs create() draws, randint accepting its first word
@@ -1758,7 +1693,6 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     const uint32_t key = uint32_t(__shfl(int(pend_key), src, 64));
     const bool hk = __shfl(int(have_key), src, 64) != 0;
     const bool ud = __shfl(int(undrawn), src, 64) != 0;
-    const int hf = __shfl(nhalf, src, 64);   // the bullet half of the env's group after this step
 
     const int uw = u < NW ? u : 0;
     uint32_t a0, a1, b0;
@@ -1832,7 +1766,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     if (on && fast) {
         if (u == 0) {   // the stream record's game seed and the header, as restart_env
             st.stream[4 * size_t(ie) + 3] = seed;
-            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, hw1(n, cf ? 2 : 0, hf, 0, 0), int(UNDRAWN), 0);
+            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | (cf ? 2 << 8 : 0), int(UNDRAWN), 0);
         }
     }
     if (on && !fast && u == 0) s_serial[L / LPE] = 1;
@@ -2101,113 +2035,37 @@ __device__ __forceinline__ void report_error(const AstroState &st, uint32_t bits
 // 295-300), in two parts so the first rounds' loads can fly during other
 // work: bullets_begin (after the header) numbers the wave's live bullets --
 // bullet k of env e is g = off_e + k, so the pass runs ceil(sum nb / 64)
-// rounds instead of max over envs of ceil(nb / LPE) -- and where each env's
-// bullets go in the other half (s_dst: the group's earlier envs' live
-// bullets and fire-tick spawn slots), writes the first index window, clears
-// the envs' LDS words and loads the first two rounds' bullets; the bullets
-// of a bullet group are contiguous, so a round's 64 lanes read ~8 lines.
-// bullets_rounds stages the envs' old bodies in LDS, collides, moves, culls
-// and compacts every live bullet into the other half, and leaves per env the
-// kept count (s_kept) and the ships the bullets hit (s_hit).
-// The wave's bullet groups (one for the quad kernel's 16 envs, two for the
-// pair kernel's 32): each group's region in the half it is read from and in
-// the half it is written to (wave-uniform; every env of a group is in the
-// same half)
-struct BulletGroups {
-    // group 0's regions and group 1's minus group 0's: a select between
-    // two values (a select between two members became an indexed load from
-    // the struct in scratch memory)
-    size_t src0, dsrc, dst0, ddst;
-    __device__ __forceinline__ size_t src_of(uint32_t w) const {
-        return src0 + (bw_env(w) >= BGROUP ? dsrc : size_t(0)) + bw_pos(w);
-    }
-    __device__ __forceinline__ size_t dst_of(uint32_t w) const { return dst0 + (bw_env(w) >= BGROUP ? ddst : size_t(0)); }
-};
-
+// rounds instead of max over envs of ceil(nb / LPE) -- writes the first
+// index window, clears the envs' LDS words and loads the first two rounds'
+// bullets; bullets_rounds stages the envs' old bodies in LDS, collides,
+// moves, culls and compacts every live bullet, and leaves per env the kept
+// count (s_kept) and the ships the bullets hit (s_hit).
 template <typename T>
 struct BulletsIn {
     int total, off;
     uint32_t tag, bw0, bw1;
-    int half0, half1;   // (wave-uniform) the half each of the wave's bullet groups is read from
     typename Store<T>::V cur0, cur1;
 };
 
-// the wave's bullet groups' regions (recomputed where needed: a few scalar
-// instructions, cheaper than holding eight SGPRs across the physics).  Every
-// operand is made wave-uniform first, so the 64-bit products are scalar
-// multiplies (from a lane value they were 64-bit vector multiplies and eight
-// readfirstlanes in front of the bullet pass)
-template <int LPE>
-__device__ __forceinline__ BulletGroups bullet_groups(const AstroState &st, const AstroParams &p, int base, int half0,
-                                                      int half1) {
-    const uint32_t bcs = uint32_t(p.b_cap + p.nships), n = uint32_t(st.n_env);
-    const uint32_t g0 = __builtin_amdgcn_readfirstlane(uint32_t(base) & ~uint32_t(BGROUP - 1));
-    const uint32_t h0 = __builtin_amdgcn_readfirstlane(uint32_t(half0));
-    auto at = [&](uint32_t h, uint32_t g) { return size_t(h ? n + g : g) * size_t(bcs); };   // bullet_base
-    BulletGroups g;
-    g.src0 = at(h0, g0);
-    g.dst0 = at(h0 ^ 1u, g0);
-    g.dsrc = g.ddst = 0;
-    if constexpr (64 / LPE > BGROUP) {   // (pair: the wave's second bullet group starts at env 16)
-        const uint32_t h1 = __builtin_amdgcn_readfirstlane(uint32_t(half1));
-        g.dsrc = at(h1, g0 + BGROUP) - g.src0;
-        g.ddst = at(h1 ^ 1u, g0 + BGROUP) - g.dst0;
-    }
-    return g;
-}
-
 template <typename T, int LPE>
-__device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroParams &p, const AstroState &st, int lane, int e,
-                                                      int q, int base, int nb, uint32_t hw, int res, bool t0,
-                                                      uint32_t *s_index, int *s_kept, int *s_hit, int *s_serial,
-                                                      int *s_dst) {
+__device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroState &st, size_t BC, int lane, int e, int q, int base,
+                                                      int nb, int np, bool t0, uint32_t *s_index, int *s_kept,
+                                                      int *s_hit, int *s_serial) {
     using V = typename Store<T>::V;
     const V *bullets = reinterpret_cast<const V *>(st.bullets);
     BulletsIn<T> b;
-    if (__builtin_amdgcn_readfirstlane(__any((nb | res) != 0)) == 0) {   // uniform: no live bullet and no
-        b.total = 0;                                                     // spawn in the wave (config 2)
-        b.off = 0;
-        b.half0 = b.half1 = __builtin_amdgcn_readfirstlane(hw1_half(hw));
-        b.tag = b.bw0 = b.bw1 = 0u;
-        b.cur0 = b.cur1 = V{};
-        if (q == 0) {
-            s_kept[e] = 0;
-            s_hit[e] = 0;
-            s_serial[e] = 0;
-            s_dst[e] = 0;
-        }
-        return b;
-    }
-    // one scan for both: the wave's live bullets (low half: their dense
-    // numbering) and, per bullet group, live bullets + the S spawn slots of
-    // the envs that fire this tick (high half: where each env's bullets go
-    // in the other half); a wave's sums are < 2^16 (nb <= b_cap <= 1000).
-    // (Reserving S slots for every env instead keeps the fire test off the
-    // scan, but the holes it leaves spread a group's reads over ~50% more
-    // lines: c3 12.07 -> 12.54 us, profiles/round4/ab_packed_bullets_v8v9.jsonl)
-    const int v = q == 0 ? nb | ((nb + res) << 16) : 0;
-    const int incl = wave_incl_scan(v, lane);
-    b.off = (incl & 0xffff) - nb;
-    int dst = (incl >> 16) - (nb + res);   // (every lane of the env)
-    // the wave's bullet groups, their halves and regions
-    b.half0 = __builtin_amdgcn_readfirstlane(hw1_half(hw));
-    b.half1 = b.half0;
-    if constexpr (64 / LPE > BGROUP) {   // (pair: the wave's second bullet group starts at env 16)
-        dst -= e >= BGROUP ? (__builtin_amdgcn_readlane(incl, BGROUP * LPE - 1) >> 16) : 0;
-        b.half1 = __builtin_amdgcn_readlane(hw1_half(hw), BGROUP * LPE);
-    }
-    const BulletGroups g = bullet_groups<LPE>(st, p, base, b.half0, b.half1);
+    const int incl = wave_incl_scan(q == 0 ? nb : 0, lane);
+    b.off = incl - nb;
 #ifdef ASTRO_ABLATE_BULLETS   // timing ablation only (wrong results)
     b.total = 0;
 #else
-    b.total = __builtin_amdgcn_readlane(incl, 63) & 0xffff;
+    b.total = __builtin_amdgcn_readlane(incl, 63);
 #endif
-    b.tag = bw_tag(e, hw1_boff(hw), t0, hw1_half(hw));
+    b.tag = bw_tag(e, np, t0);
     if (q == 0) {
         s_kept[e] = 0;
         s_hit[e] = 0;
         s_serial[e] = 0;
-        s_dst[e] = dst;
     }
     if (b.total == 0) {   // uniform: no live bullet in the wave (config 2): no index, no loads
         b.bw0 = b.bw1 = 0u;
@@ -2218,8 +2076,8 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroParams &p, cons
     wave_sync();
     b.bw0 = lane < b.total ? s_index[lane] : 0u;
     b.bw1 = lane + 64 < min(b.total, QWIN) ? s_index[lane + 64] : 0u;
-    b.cur0 = bullets[g.src_of(b.bw0)];
-    b.cur1 = bullets[g.src_of(b.bw1)];
+    b.cur0 = bullets[size_t(base + bw_env(b.bw0)) * BC + bw_slot(b.bw0)];
+    b.cur1 = bullets[size_t(base + bw_env(b.bw1)) * BC + bw_slot(b.bw1)];
     return b;
 }
 
@@ -2232,18 +2090,17 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
                                                const float (&syf)[S], const float (&mpxf)[PMAX / LPE],
                                                const float (&mpyf)[PMAX / LPE],
                                                float4 (*s_body)[(S + PMAX + 1) / 2], uint32_t *s_index,
-                                               int *s_kept, int *s_hit, const int *s_dst, const Guard &gp,
-                                               const Guard &gs STAMP_ARG) {
+                                               int *s_kept, int *s_hit, const Guard &gp, const Guard &gs STAMP_ARG) {
     using V = typename Store<T>::V;
     constexpr int PPL = PMAX / LPE;
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
     const size_t NN = size_t(st.n_env);
+    const size_t BC = size_t(p.b_cap);
     const V *ships = reinterpret_cast<const V *>(st.ships);
     const V *planets = reinterpret_cast<const V *>(st.planets);
     V *bullets = reinterpret_cast<V *>(st.bullets);
     const int total = b.total, off = b.off;
     const uint32_t tag = b.tag;
-    const BulletGroups g = bullet_groups<LPE>(st, p, base, b.half0, b.half1);
     uint32_t bw0 = b.bw0, bw1 = b.bw1;
     V cur0 = b.cur0, cur1 = b.cur1;
     if (total == 0) {   // uniform: nothing to do (bullets_begin left s_kept, s_hit cleared)
@@ -2264,14 +2121,15 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
     wave_sync();
     STAMP(16);
     // lane g of a round takes live bullet r0 + g of the wave: collide with the
-    // OLD bodies, move, cull, and compact in slot order within its env into
-    // the other half (the group's region there, after s_dst[env] entries)
+    // OLD bodies, move, cull, and compact in slot order within its env, in
+    // place (a bullet is only ever written to a slot <= the one it was read
+    // from, and every slot is read before any later round writes)
     {
         const uint64_t lanes_below = (1ull << lane) - 1;
         const double dt = p.dt;
         int kept_before = 0;   // kept bullets of the wave in earlier rounds
         int carry = 0;         // kept_before at the start of the env spanning into the next round
-        for (int w0 = 0; w0 < total; w0 += QWIN) {   // uniform; one window unless > 32 bullets/env
+        for (int w0 = 0; w0 < total; w0 += QWIN) {   // uniform; one window unless > 64 bullets/env
           const int wend = min(total, w0 + QWIN);
           if (w0 > 0) {
               wave_sync();   // the previous window is read
@@ -2279,8 +2137,8 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
               wave_sync();
               bw0 = w0 + lane < wend ? s_index[lane] : 0u;
               bw1 = w0 + 64 + lane < wend ? s_index[64 + lane] : 0u;
-              cur0 = bullets[g.src_of(bw0)];
-              cur1 = bullets[g.src_of(bw1)];
+              cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
+              cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
           }
           // one round: lane g takes live bullet r0 + g (index word bw, data cur)
           // NR rounds at once, lane g of round r taking live bullet r0 + 64 r + g
@@ -2332,13 +2190,12 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
                   for (int r = 0; r < NR; ++r) {
                       if (amb[r]) {
                           const size_t ie = size_t(base + be[r]);
+                          const int bnp = bw_np(bws[r]);
                           const double x = double(curs[r].x), y = double(curs[r].y);
                           bool bh64 = false;
 #pragma unroll
                           for (int j = 0; j < PMAX; ++j) {
-                              // a live planet slot: its LDS copy is not parked at -FAR_POS
-                              const float4 v = s_body[be[r]][(S + j) / 2];
-                              if (((S + j) & 1 ? v.z : v.x) != -FAR_POS) {
+                              if (j < bnp) {
                                   const V pj = planets[size_t(j) * NN + ie];
                                   bh64 |= closer_exact(x, y, double(pj.x), double(pj.y), gp, bt0[r]);
                               }
@@ -2401,7 +2258,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
                       }
                   }
               }
-              // compaction in slot order, round by round, into the other half
+              // compaction in slot order, round by round
 #pragma unroll
               for (int r = 0; r < NR; ++r) {
                   const bool kp = keep[r] & valid[r] & !bh[r];
@@ -2410,7 +2267,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
                   const int first = lane - bw_slot(bws[r]);   // lane of the env's slot 0 (< 0: an earlier round)
                   const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
                   const int pos = kg - k0;
-                  if (kp) st_out(&bullets[g.dst_of(bws[r]) + size_t(s_dst[be[r]] + pos)], out[r]);
+                  if (kp) st_out(&bullets[size_t(base + be[r]) * BC + pos], out[r]);
                   if (valid[r] && bw_last(bws[r])) s_kept[be[r]] = pos + int(kp);
                   carry = __builtin_amdgcn_readlane(k0, 63);
                   kept_before += __popcll(kb);
@@ -2428,11 +2285,12 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           // latency sets, with helper waves or K ticks); with 8 the registers
           // of two rounds spill (measured: c5 30.8 -> 34.3 us), and the
           // one-tick instances without helpers (millions of envs, HBM-bound)
-          // keep the registers for occupancy instead: one at a time
+          // keep the registers for occupancy instead (c3 at 1M envs 128.3 ->
+          // 114.0 us, profiles/round4/ab_packed_bullets_v8v9.jsonl): one at a time
           constexpr int NR2 = PMAX <= 4 ? NRW : 1;
           if (nr >= 3) {
               bws[2] = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
-              curs[2] = bullets[g.src_of(bws[2])];
+              curs[2] = bullets[size_t(base + bw_env(bws[2])) * BC + bw_slot(bws[2])];
           }
           if (nr >= 2) {
               rounds(std::integral_constant<int, NR2>(), w0, bws, curs);
@@ -2444,7 +2302,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           if (nr >= 3) rounds(std::integral_constant<int, 1>(), w0 + 128, bws + 2, curs + 2);
           for (int r0 = w0 + 192; r0 < wend; r0 += 64) {   // uniform; rare
               const uint32_t bw = r0 + lane < wend ? s_index[r0 + lane - w0] : 0u;
-              const V cur = bullets[g.src_of(bw)];
+              const V cur = bullets[size_t(base + bw_env(bw)) * BC + bw_slot(bw)];
               rounds(std::integral_constant<int, 1>(), r0, &bw, &cur);
           }
         }
@@ -2464,7 +2322,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // LDS, one set per wave of the workgroup
     __shared__ float4 s_body_all[WPG][QENV][NBOD2];       // float32 (x, y): ships, then planets (padding far)
     __shared__ uint32_t s_index_all[WPG][QWIN];           // a window of the wave's live bullets, see bw_*
-    __shared__ int s_dst_all[WPG][QENV];                  // where each env's bullets go (bullets_begin)
     __shared__ int s_kept_all[WPG][QENV], s_hit_all[WPG][QENV], s_serial_all[WPG][QENV];
     __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
     __shared__ HelpBox s_box_all[HELP ? WPG : 1];
@@ -2477,7 +2334,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // step waves are the critical path (c2 5.36 -> 5.20 us A/B); in the pair
     // instance the helpers' resets are the tail (c3 12.19 -> 12.52 us)
     constexpr bool PENDING_ON_HELPER = HELP && LPE == 4;
-    __shared__ uint4 s_cpend_all[HELP && !PENDING_ON_HELPER ? WPG : 1][HELP && !PENDING_ON_HELPER ? QENV : 1];   // see c_pend
     // the planet update on the helpers: pair instance only (the quad instance
     // of c2 lost with it there: 5.08 -> 5.33 us, ab_quad_planets_on_helper.jsonl)
     constexpr bool PLANETS_ON_HELPER = HELP && LPE == 2;
@@ -2485,7 +2341,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
     float4 (*s_body)[NBOD2] = s_body_all[wv];
     uint32_t *s_index = s_index_all[wv];
-    int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv], *s_dst = s_dst_all[wv];
+    int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv];
     uint32_t (*s_chain)[2][13 + 2 * S] = s_chain_all[wv];
 
     const int N = st.n_env;
@@ -2525,23 +2381,10 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             // its end: it waits for this word, so the header read here is the
             // launch's input whatever the memory system's timing (the store
             // depends on the loaded value: it waits for the load's return)
+            if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
             const uint32_t hseed = uint32_t(hh.z) & SEED_MASK;
             const bool kvalid = (uint32_t(hh.z) & KEY_VALID) != 0;
             const bool hud = (uint32_t(hh.z) & UNDRAWN) != 0;   // (a reset then takes the serial path)
-            if constexpr (!PENDING_ON_HELPER) {
-                // the stream cursor the step wave's pending-seed check
-                // (check_pending, at its end) needs, into LDS: the step wave
-                // does not hold it in registers across its bullet pass (it
-                // spilled) nor waits for it anywhere; `seen` (below) orders it
-                // before the step wave's read
-                const bool want_c = q == 0 && (hud || (!kvalid && p.key_table && p.planets_only));
-                uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
-                asm volatile("" : "+s"(c_stream), "+s"(c_hdr));
-                const uint4 c = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
-                if (q == 0) s_cpend_all[wv][e] = c;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the cursor before the flag)
-            }
-            if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
             uint32_t hkey = uint32_t(hh.w);
             const bool hk = kvalid || p.key_table != nullptr;
             if (q == 1 && !kvalid && !hud) hkey = p.key_table ? p.key_table[hseed & SEED_MASK] : mt_key_at(hseed, 0, MT_PROLOGUE);
@@ -2584,9 +2427,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             const size_t NN = size_t(N);
             V *planets = reinterpret_cast<V *>(st.planets);
             constexpr int PPL = PMAX / LPE;
-            int np = hw1_np(uint32_t(hh.y));
+            int np = hh.y & 0xff;
             np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
-            const int hnhalf = hw1_half(uint32_t(hh.y)) ^ 1;   // the envs' bullet half after this step
             const bool t0 = (uint32_t(hh.x) & TICK_MASK) == 0;
             const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
             V hpv[PPL], hout[PPL];
@@ -2641,15 +2483,15 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             if (todo0) {   // uniform
 #endif
                 for (uint64_t todo = todo0; todo;)   // uniform
-                    todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, hud, hnhalf,
-                                                                  s_chain, s_serial STAMP_PASS, pre);
+                    todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, hud, s_chain,
+                                                                  s_serial STAMP_PASS, pre);
                 wave_sync();
                 if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
                 if (active && s_serial[e]) {   // uniform over the quad; rare
                     const uint32_t kq = uint32_t(quad_bcast_i<1, LPE>(int(hkey)));   // (lane q == 1 has the key)
                     const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
                     const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, hud, c, stream_ring_of(st, i));
-                    restart_env<T, S, PMAX, LPE>(p, st, i, ng, hnhalf, q);
+                    restart_env<T, S, PMAX, LPE>(p, st, i, ng, q);
                 }
             }
 #ifdef ASTRO_STAMPS
@@ -2659,6 +2501,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             return hc;
         }
     }
+    const size_t BC = size_t(p.b_cap);
     V *ships = reinterpret_cast<V *>(st.ships);
     T *ships_b = reinterpret_cast<T *>(st.ships_b);
     V *planets = reinterpret_cast<V *>(st.planets);
@@ -2707,10 +2550,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const bool key_valid = (uint32_t(h.z) & KEY_VALID) != 0;
     const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
     uint32_t pend_seed = uint32_t(h.z) & SEED_MASK;
-    const uint32_t hw = uint32_t(h.y);
-    int np = hw1_np(hw);
-    const int flags = hw1_flags(hw);
-    const int nb = active ? min(hw1_nb(hw), p.b_cap) : 0;
+    int np = h.y & 0xff;
+    const int flags = (h.y >> 8) & 0xff;
+    const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
     np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
     if constexpr (PLANETS_AFTER_HDR) {
 #pragma unroll
@@ -2738,18 +2580,13 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const bool live = tick < p.timeout_tick;
     const bool t0 = tick == 0;
     STAMP(1);
-    const bool fires = fires_at(p, tick, live);
+    const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
     uint32_t pend_key = uint32_t(h.w);
     n_pl += active && q == 0 ? uint32_t(np) : 0u;
 
-    // ---- index the wave's live bullets densely and place each env's bullets
-    //      in the other half (bullets_begin); their first two rounds load
-    //      during the physics below
-    const BulletsIn<T> bin = bullets_begin<T, LPE>(p, st, lane, e, q, base, nb, hw, active && fires ? S : 0, t0,
-                                                   s_index, s_kept, s_hit, s_serial, s_dst);
-    // the env's bullet group's half (this step writes the other): from the
-    // wave-uniform values, not held per lane
-    auto half_of_env = [&]() { return e >= BGROUP ? bin.half1 : bin.half0; };
+    // ---- index the wave's live bullets densely (bullets_begin); their first
+    //      two rounds load during the physics below
+    const BulletsIn<T> bin = bullets_begin<T, LPE>(st, BC, lane, e, q, base, nb, np, t0, s_index, s_kept, s_hit, s_serial);
     const int total = bin.total;
     STAMP(19);
     // key[397] of the next game's seed (first step of a game): a random
@@ -2770,11 +2607,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #else
     const bool want_c = !PENDING_ON_HELPER && q == 0 && (undrawn || (!key_valid && p.key_table && p.planets_only));
 #endif
-    // (with helper waves, the helper loads it into LDS: s_cpend)
     uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
     asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // values, not a select between the fields' addresses
-    uint4 c_pend = make_uint4(0u, 0u, 0u, 0u);
-    if constexpr (!HELP) c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
+    const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
 
     // ---- quad broadcasts: all planets, both ships
     double px[PMAX], py[PMAX], sx[S], sy[S];
@@ -2930,15 +2765,14 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 
     STAMP(3);
     // ---- bullets (core.py:241-251, 264-266, 295-300): collide with the old
-    //      bodies, move, cull, compact into the other half (bullets_rounds)
-    bullets_rounds<T, S, PMAX, LPE, (HELP || OPAQUE) ? 2 : 1>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf, s_body, s_index, s_kept,
-                                    s_hit, s_dst, gp, gs STAMP_PASS);
+    //      bodies, move, cull, compact in place (bullets_rounds)
+    bullets_rounds<T, S, PMAX, LPE, (HELP || OPAQUE) ? 2 : 1>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf,
+                                                              s_body, s_index, s_kept, s_hit, gp, gs STAMP_PASS);
     if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
         if (!wait_lds_word(s_box_all[wv].seen)) report_error(st, ASTRO_ERR_HEADER_WAIT, lane);
     }
     const int wr_in = s_kept[e];
     const int hit_bits = s_hit[e];
-    const int dst_off = s_dst[e];   // the env's first entry in its group's region of the other half
     // the stores below recompute their addresses from an opaque copy of the
     // env index (holding the load addresses live across the bullet pass
     // costs registers the bullet pass needs)
@@ -2969,7 +2803,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         if (!done) {   // uniform over the quad
             // ---- fire: ship s's bullet appended after the survivors, in ship order
             int wr = wr_in;
-            if (fires) {
+            if ((fire_word >> (tick & 31)) & 1u) {
                 bool keep = false;
                 V out;
                 if (q < S) {
@@ -2998,9 +2832,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 }
                 const uint64_t nib = (__ballot(keep) >> (lane & ~(LPE - 1))) & ((1ull << LPE) - 1);
                 const int pos = wr + __popcll(nib & ((1ull << q) - 1));
-                if (keep && pos < p.b_cap)
-                    st_out(&bullets[bullet_groups<LPE>(st, p, base, bin.half0, bin.half1).dst_of(uint32_t(e)) +
-                                    size_t(dst_off + pos)], out);
+                if (keep && pos < p.b_cap) st_out(&bullets[size_t(is) * BC + pos], out);
                 wr += __popcll(nib);
             }
             const int w = wr < p.b_cap ? wr : p.b_cap;
@@ -3034,19 +2866,16 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             STAMP(7);
             if (q == 0) {
                 const int fl = flags | (dropped ? 1 : 0);
-                const int w1 = hw1(np, fl, half_of_env() ^ 1, w, dst_off);
                 if constexpr (PENDING_ON_HELPER) {   // words 2-3: the helper's
-                    st_out(&reinterpret_cast<int2 *>(st.hdr)[2 * is], make_int2(tick + 1, w1));
+                    st_out(&reinterpret_cast<int2 *>(st.hdr)[2 * is], make_int2(tick + 1, np | (fl << 8) | (w << 16)));
                 } else {
 #ifdef ASTRO_ABLATE_PENDING
                     const uint32_t kv = key_valid ? KEY_VALID : 0u;
 #else
-                    // (the stream cursor: its helper's copy in LDS, see s_cpend)
-                    const uint32_t kv = check_pending(p, st, is, key_valid, undrawn,
-                                                      HELP ? s_cpend_all[HELP ? wv : 0][HELP ? e : 0] : c_pend,
-                                                      pend_seed, pend_key);
+                    const uint32_t kv = check_pending(p, st, is, key_valid, undrawn, c_pend, pend_seed, pend_key);
 #endif
-                    st_out(&reinterpret_cast<int4 *>(st.hdr)[is], make_int4(tick + 1, w1, int(pend_seed | kv), int(pend_key)));
+                    st_out(&reinterpret_cast<int4 *>(st.hdr)[is],
+                           make_int4(tick + 1, np | (fl << 8) | (w << 16), int(pend_seed | kv), int(pend_key)));
                 }
                 n_bout += uint32_t(w);
                 n_drop += uint32_t(dropped);
@@ -3058,8 +2887,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             f_tout = q == 0 && timeout;
             need_reset = auto_reset && q == 0;
             f_reset = need_reset;
-            if (!auto_reset && q == 0)   // no bullets, and in the group's new half (the rest is left for astro_reset)
-                reinterpret_cast<int *>(st.hdr)[4 * size_t(is) + 1] = hw1(np, flags, half_of_env() ^ 1, 0, 0);
         }
     }
 
@@ -3069,7 +2896,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     if constexpr (!HELP)
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
         todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
-                                                undrawn, half_of_env() ^ 1, s_chain, s_serial STAMP_PASS);
+                                           undrawn, s_chain, s_serial STAMP_PASS);
     if (!HELP && auto_reset) {
         wave_sync();
         if (stats) c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));
@@ -3078,7 +2905,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
             const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, undrawn, c,
                                                 stream_ring_of(st, is));
-            restart_env<T, S, PMAX, LPE>(p, st, is, ng, half_of_env() ^ 1, q);
+            restart_env<T, S, PMAX, LPE>(p, st, is, ng, q);
         }
     }
     STAMP(10);
@@ -3143,8 +2970,8 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 // Waves per SIMD the one-tick instances without helpers are built for:
 // 8 planet slots: 3 (141 VGPRs, no spills; at 4: 128 VGPRs, 41 spilled, c5
-// 34.3 -> 31.1 us); 4 slots: 3 (135 VGPRs, no spills; at 4: 7 spilled, c3 at
-// 1M envs 139.6 -> 127.1 us, at 256k 39.5 -> 37.3 us, ab_p4_waves.jsonl)
+// 34.3 -> 31.1 us); 4 slots: 3 (at 4: no gain, c3 at 1M envs 114.0 vs
+// 114.3 us, profiles/round4/ab_packed_bullets_v8v9.jsonl).
 // The K-tick (rollout) instances: 4 planet slots at 3 waves per SIMD (168
 // VGPRs; at 2 the 1M-env rollouts ran 110 vs 91 us per tick,
 // profiles/round4/ab_packed_bullets_v1.jsonl), 8 slots and the ScriptBot
@@ -3242,7 +3069,6 @@ __global__ __launch_bounds__(FEAT_BLOCK) void astro_features_kernel(AstroParams 
     constexpr int MAXE = FEAT_BLOCK + 1;   // envs a block can touch (rows >= 1)
     __shared__ float s_ship[MAXE][5 * S];
     __shared__ int s_cnt[MAXE][2];         // nplanets, nbullets
-    __shared__ size_t s_boff[MAXE];        // the env's first live bullet (entries from st.bullets)
     __shared__ float4 s_out[FEAT_BLOCK * D / 4 + 1];
     const int N = st.n_env;
     const size_t NN = size_t(N);
@@ -3258,11 +3084,9 @@ __global__ __launch_bounds__(FEAT_BLOCK) void astro_features_kernel(AstroParams 
         const int le = k / S, s = k - le * S, i = e0 + le;
         const int4 h = reinterpret_cast<const int4 *>(st.hdr)[i];
         if (s == 0) {
-            const uint32_t hw = uint32_t(h.y);
-            const int np = hw1_np(hw);
+            int np = h.y & 0xff;
             s_cnt[le][0] = np < 1 ? 1 : (np > p.p_pad ? p.p_pad : np);
-            s_cnt[le][1] = min(hw1_nb(hw), p.b_cap);
-            s_boff[le] = bullet_base(st, p, hw1_half(hw), i) + size_t(hw1_boff(hw));
+            s_cnt[le][1] = min(int(uint32_t(h.y) >> 16), p.b_cap);
         }
         const bool t0 = (uint32_t(h.x) & TICK_MASK) == 0;
         const V v = reinterpret_cast<const V *>(st.ships)[size_t(s) * NN + i];
@@ -3290,7 +3114,7 @@ __global__ __launch_bounds__(FEAT_BLOCK) void astro_features_kernel(AstroParams 
 #pragma unroll
             for (int k = 0; k < 5 * S; ++k) f[1 + k] = s_ship[le][k];
             const V o = r < np ? reinterpret_cast<const V *>(st.planets)[size_t(r) * NN + i]
-                               : reinterpret_cast<const V *>(st.bullets)[s_boff[le] + size_t(r - np)];
+                               : reinterpret_cast<const V *>(st.bullets)[size_t(i) * size_t(p.b_cap) + (r - np)];
             f[1 + 5 * S] = float(o.x);
             f[2 + 5 * S] = float(o.y);
             f[3 + 5 * S] = float(o.z);
@@ -3330,17 +3154,15 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
         const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
         const uint32_t key = (uint32_t(h.z) & KEY_VALID) ? uint32_t(h.w) : undrawn ? 0u : key397_of(p, seed);
         const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, undrawn, c, stream_ring_of(st, i)),
-                                hw1_half(uint32_t(h.y)));
+        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, undrawn, c, stream_ring_of(st, i)));
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued
     int cf = 0;
     const uint32_t seed = seeds[i];
     const int n = create_env<T, S, PMAX>(p, st, i, create_draws<S>(create_words<S>(p, seed, key397_of(p, seed))), cf);
-    // (the env's bullet group keeps its half: the other envs' bullets stay where they are)
     reinterpret_cast<int4 *>(st.hdr)[i] =
-        make_int4(int(uint32_t(h.x) & ~TICK_MASK), hw1(n, cf ? 2 : 0, hw1_half(uint32_t(h.y)), 0, 0), h.z, h.w);
+        make_int4(int(uint32_t(h.x) & ~TICK_MASK), n | ((cf ? 2 : 0) << 8), h.z, h.w);
     if (st.stream) reinterpret_cast<uint32_t *>(st.stream)[4 * i + 3] = seed;
 }
 
@@ -3416,11 +3238,9 @@ int check_params(const AstroParams *p) {
     if (p->p_pad < 1 || p->p_pad > 16) return fail(-13, "p_pad must be in [1, 16]");
     if (p->max_planets < 1 || p->max_planets > p->p_pad)
         return fail(-14, "max_planets must be in [1, p_pad]");
-    if (p->b_cap < 1 || p->b_cap > ASTRO_MAX_B_CAP) return fail(-15, "b_cap must be in [1, %d]", ASTRO_MAX_B_CAP);
+    if (p->b_cap < 1 || p->b_cap > 65535) return fail(-15, "b_cap must be in [1, 65535]");
     if (p->timeout_tick < 0 || p->timeout_tick >= int(TICK_MASK)) return fail(-16, "timeout_tick out of [0, 2^22)");
-    if (p->timeout_tick > 0 && !p->fire_bits && p->fire_period <= 0) return fail(-17, "fire_bits is NULL");
-    if (p->fire_period > 0 && (p->fire_phase < 0 || p->fire_phase >= p->fire_period))
-        return fail(-17, "fire_phase must be in [0, fire_period)");
+    if (p->timeout_tick > 0 && !p->fire_bits) return fail(-17, "fire_bits is NULL");
     if (p->kernel < 0 || p->kernel > 3) return fail(-18, "kernel must be 0 (auto), 1 (lane), 2 (quad) or 3 (pair)");
     if (p->planets_only < 0 || p->planets_only > p->max_planets)
         return fail(-19, "planets_only must be in [0, max_planets]");

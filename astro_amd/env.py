@@ -11,17 +11,14 @@ tick and, for games that end, starts the env's next game in the same kernel
 (``env_offset``) plays exactly the games of a 1-GPU run.
 
 All state lives in HBM as PyTorch tensors; ships and planets struct-of-arrays,
-entity-major (a wave's lanes read contiguous rows), bullets packed per bullet
-group of 16 envs in two halves (a step reads a group's live bullets from one
-half, contiguous, and writes them to the other; ``bullet_rows()`` gives them
-as per-env rows):
+entity-major (a wave's lanes read contiguous rows), bullets one contiguous row
+per env (the kernels walk an env's live bullets in slot order):
 
     ships    [S, N, 4]   x, y, dx, dy        ships_b  [S, N]
-    planets  [P, N, 4]   x, y, dx, dy        bullets  [2, N * (B + S), 4]
-    hdr      [N, 4]      tick, nplanets | flags << 5 | half << 7 | nbullets << 8
-                         | boff << 18, next game's seed | key_valid << 31 (or
-                         undrawn << 30: the game's first step draws it), key[397]
-                         of its init chain
+    planets  [P, N, 4]   x, y, dx, dy        bullets  [N, B, 4]
+    hdr      [N, 4]      tick, nplanets | flags << 8 | nbullets << 16,
+                         next game's seed | key_valid << 31 (or undrawn << 30: the
+                         game's first step draws it), key[397] of its init chain
     stream   [N, 4]      seed-stream cursor + current game's seed
     stream_ring [N, 624] the stream's MT19937 state words (exact for any length)
 
@@ -42,60 +39,6 @@ from . import schedule as _schedule
 
 TICK_MASK = (1 << 22) - 1
 MT_N = 624   # MT19937 state words: each env's seed stream keeps its own (stream_ring)
-MAX_B_CAP = 1000      # include/astro_step.h ASTRO_MAX_B_CAP
-BULLET_GROUP = 16     # include/astro_step.h ASTRO_BULLET_GROUP
-
-
-def hdr_word1(nplanets, flags, half, nbullets, boff):
-    """hdr word 1 (include/astro_step.h) from its fields (numpy int64 arrays
-    or ints), as uint32."""
-    w = (np.asarray(nplanets, np.int64) | (np.asarray(flags, np.int64) << 5) | (np.asarray(half, np.int64) << 7)
-         | (np.asarray(nbullets, np.int64) << 8) | (np.asarray(boff, np.int64) << 18))
-    return (w & 0xFFFFFFFF).astype(np.uint32)
-
-
-def group_offsets(nbullets):
-    """Packed placement of per-env bullet counts: each env's first entry in
-    its bullet group's region (the group's earlier envs' counts summed)."""
-    nb = np.asarray(nbullets, np.int64)
-    n = nb.size
-    g = np.zeros(-(-n // BULLET_GROUP) * BULLET_GROUP, np.int64)
-    g[:n] = nb
-    g = g.reshape(-1, BULLET_GROUP)
-    return (np.cumsum(g, 1) - g).reshape(-1)[:n]
-
-
-def pack_bullets(rows, nbullets, nships):
-    """Per-env bullet rows [N, >= max nbullets, 4] -> (packed [2, N * (b_cap +
-    S), 4] with every group in half 0, boff [N]) for b_cap = rows' width."""
-    rows = np.asarray(rows)
-    nb = np.asarray(nbullets, np.int64)
-    n, b_cap = rows.shape[0], rows.shape[1]
-    bcs = b_cap + nships
-    boff = group_offsets(nb)
-    k = np.arange(b_cap)
-    live = k[None, :] < nb[:, None]
-    start = (np.arange(n) // BULLET_GROUP) * (BULLET_GROUP * bcs) + boff
-    packed = np.zeros((2, n * bcs, 4), rows.dtype)
-    packed[0, (start[:, None] + k[None, :])[live]] = rows[live]
-    return packed, boff
-
-
-def bullet_rows_of(bullets, hdr_word1s, b_cap, nships):
-    """The gather behind BatchedEnv.bullet_rows (torch, any device): packed
-    halves [2, N * (b_cap + S), 4] and hdr word 1 [N] -> rows [N, b_cap, 4],
-    zeros past each env's live bullets."""
-    w1 = hdr_word1s.to(torch.int64) & 0xFFFFFFFF
-    n, dev = w1.shape[0], w1.device
-    bcs = b_cap + nships
-    nb = (w1 >> 8) & 0x3ff
-    i = torch.arange(n, device=dev, dtype=torch.int64)
-    start = ((w1 >> 7) & 1) * (n * bcs) + (i // BULLET_GROUP) * (BULLET_GROUP * bcs) + ((w1 >> 18) & 0x3fff)
-    k = torch.arange(b_cap, device=dev, dtype=torch.int64)
-    live = k[None, :] < nb[:, None]
-    idx = torch.where(live, start[:, None] + k[None, :], torch.zeros((), dtype=torch.int64, device=dev))
-    rows = bullets.reshape(-1, 4)[idx]
-    return torch.where(live[..., None], rows, torch.zeros((), dtype=rows.dtype, device=dev))
 
 Observation = collections.namedtuple(
     'Observation', ('ships', 'ships_b', 'planets', 'nplanets', 'bullets', 'nbullets', 'tick'))
@@ -203,8 +146,6 @@ class BatchedEnv:
         if self.p_pad < config.max_planets or self.p_pad > 16:
             raise ValueError('p_pad must be in [max_planets, 16]')
         self.b_cap = int(b_cap)
-        if not 1 <= self.b_cap <= MAX_B_CAP:
-            raise ValueError('b_cap must be in [1, %d]' % MAX_B_CAP)
         self.dtype = dtype
         self.device = torch.device(device if device is not None else 'cuda')
         if self.device.type != 'cuda':
@@ -222,7 +163,7 @@ class BatchedEnv:
         self.ships = zs(S, N, 4)
         self.ships_b = zs(S, N)
         self.planets = zs(self.p_pad, N, 4)
-        self.bullets = zs(2, N * (self.b_cap + S), 4)   # two halves, packed per bullet group
+        self.bullets = zs(N, self.b_cap, 4)
         self.hdr = zs(N, 4, dt=torch.int32)
         self.reward = zs(N, S, dt=torch.float32)
         self.done = zs(N, dt=torch.uint8)
@@ -234,12 +175,10 @@ class BatchedEnv:
 
         k = _schedule.kernel_constants(config)
         self.key_table = key_table(dev) if use_key_table else None
-        period, phase = self.schedule.fire_period()
         self.params = _lib.AstroParams(
             p_pad=self.p_pad, b_cap=self.b_cap, timeout_tick=self.schedule.timeout_tick,
             fire_bits=self.fire_bits.data_ptr(), kernel=_lib.KERNELS[kernel], planets_only=planets_only,
-            key_table=self.key_table.data_ptr() if self.key_table is not None else None,
-            fire_period=period, fire_phase=phase, **k)
+            key_table=self.key_table.data_ptr() if self.key_table is not None else None, **k)
         self.state = _lib.AstroState(
             ships=self.ships.data_ptr(), ships_b=self.ships_b.data_ptr(),
             planets=self.planets.data_ptr(), bullets=self.bullets.data_ptr(),
@@ -352,31 +291,15 @@ class BatchedEnv:
 
     @property
     def nplanets(self):
-        return self.hdr[:, 1] & 0x1f
+        return self.hdr[:, 1] & 0xff
 
     @property
     def flags(self):
-        return (self.hdr[:, 1] >> 5) & 3
+        return (self.hdr[:, 1] >> 8) & 0xff
 
     @property
     def nbullets(self):
-        return (self.hdr[:, 1] >> 8) & 0x3ff
-
-    @property
-    def bullet_half(self):
-        """The bullet half each env's group is in (0 or 1)."""
-        return (self.hdr[:, 1] >> 7) & 1
-
-    @property
-    def bullet_offset(self):
-        """Each env's first live bullet in its group's region (entries)."""
-        return (self.hdr[:, 1] >> 18) & 0x3fff
-
-    def bullet_rows(self):
-        """Every env's live bullets as rows: [N, b_cap, 4] (x, y, dx, dy), env
-        i's in rows [0, nbullets[i]), zeros after -- a gather from the packed
-        halves (device ops, no synchronisation)."""
-        return bullet_rows_of(self.bullets, self.hdr[:, 1], self.b_cap, self.S)
+        return (self.hdr[:, 1] >> 16) & 0xffff
 
     def launch_waves(self):
         """(step waves, helper waves) of one astro_step launch of this batch:
@@ -426,12 +349,11 @@ class BatchedEnv:
         return self.stream[:, 3]
 
     def obs(self):
-        """Env-major views of the state: ships [N, S, 4] ... (views, no copies),
-        bullets [N, b_cap, 4] (bullet_rows: a gather)."""
+        """Env-major views of the state (no copies): ships [N, S, 4] ..."""
         return Observation(
             ships=self.ships.permute(1, 0, 2), ships_b=self.ships_b.permute(1, 0),
             planets=self.planets.permute(1, 0, 2), nplanets=self.nplanets,
-            bullets=self.bullet_rows(), nbullets=self.nbullets, tick=self.tick)
+            bullets=self.bullets, nbullets=self.nbullets, tick=self.tick)
 
     def policy(self, policy, seed=0, tick0=0, script_args=None):
         """The AstroPolicy of a policy name: 'random' (bench.py's splitmix64
@@ -576,7 +498,7 @@ class BatchedEnv:
         return dict(ships=self.ships.permute(1, 0, 2).cpu().numpy(),
                     ships_b=self.ships_b.permute(1, 0).cpu().numpy(),
                     planets=self.planets.permute(1, 0, 2).cpu().numpy(),
-                    bullets=self.bullet_rows().cpu().numpy(),
+                    bullets=self.bullets.cpu().numpy(),
                     tick=self.tick.cpu().numpy(), nplanets=self.nplanets.cpu().numpy(),
                     nbullets=self.nbullets.cpu().numpy(), flags=self.flags.cpu().numpy())
 
@@ -594,22 +516,19 @@ class BatchedEnv:
         pl = np.zeros((self.n_env, self.p_pad, 4))
         pl[:, :np.asarray(planets).shape[1]] = planets
         put(self.planets, pl.transpose(1, 0, 2))
+        bl = np.zeros((self.n_env, self.b_cap, 4))
+        bsrc = np.asarray(bullets)
+        nbmax = min(bsrc.shape[1], self.b_cap)
+        bl[:, :nbmax] = bsrc[:, :nbmax]
+        put(self.bullets, bl)
         nb = np.asarray(nbullets, dtype=np.int64)
         if (nb > self.b_cap).any():
             raise ValueError('a state holds more bullets than b_cap')
-        # packed into half 0: each group's envs one after the other
-        N = self.n_env
-        rows = np.zeros((N, self.b_cap, 4))
-        bsrc = np.asarray(bullets)
-        w = min(bsrc.shape[1], self.b_cap)
-        rows[:, :w] = bsrc[:, :w]
-        packed, boff = pack_bullets(rows, nb, self.S)
-        put(self.bullets, packed)
         old = self.hdr.cpu().numpy().view(np.uint32).astype(np.int64)
         hdr = old.copy()
         hdr[:, 0] = (old[:, 0] & ~TICK_MASK & 0xFFFFFFFF) | np.asarray(tick, np.int64)
-        fl = np.zeros(N, np.int64) if flags is None else np.asarray(flags, np.int64) & 3
-        hdr[:, 1] = hdr_word1(nplanets, fl, 0, nb, boff)
+        fl = np.zeros(self.n_env, np.int64) if flags is None else np.asarray(flags, np.int64) & 0xff
+        hdr[:, 1] = np.asarray(nplanets, np.int64) | (fl << 8) | (nb << 16)
         self.hdr.copy_(torch.as_tensor(hdr.astype(np.uint32).view(np.int32)).to(dev))
 
     def state_of(self, i, host=None):

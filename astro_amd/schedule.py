@@ -23,22 +23,6 @@ class Schedule:
     t: np.ndarray           # float64[timeout_tick + 1]: t before step call k
     reload: np.ndarray      # float64[timeout_tick + 1]: reload before step call k
 
-    def fire_period(self):
-        """(period, phase) when the schedule is exactly "fire on tick k iff
-        k % period == phase" for every tick before the timeout (the kernel
-        then needs no table load), else (0, 0).  A schedule that never fires
-        is period 2^30, phase 2^30 - 1."""
-        k = np.nonzero(self.fire)[0]
-        n = self.timeout_tick
-        if k.size == 0:
-            return (1 << 30, (1 << 30) - 1)
-        period = int(k[1] - k[0]) if k.size > 1 else n + 1
-        phase = int(k[0])
-        if period < 1 or phase >= period:
-            return (0, 0)
-        want = (np.arange(n) % period) == phase
-        return (period, phase) if np.array_equal(want, self.fire) else (0, 0)
-
     def fire_bits(self):
         """uint32 words, bit (k & 31) of word k >> 5 = fire on tick k."""
         n = max(1, (self.timeout_tick + 31) // 32)

@@ -32,8 +32,8 @@
  *     last failure of the calling thread.
  *   - Ships and planets are struct-of-arrays, entity-major: slot s of env i
  *     lives at [s * n_env + i], so consecutive lanes (envs) touch consecutive
- *     bytes; bullets are packed per bullet group of 16 envs (AstroState).
- *     Element type is float (state_f64 = 0) or double (state_f64 = 1).
+ *     bytes; bullets are one contiguous row per env.  Element type is float
+ *     (state_f64 = 0) or double (state_f64 = 1).
  */
 #ifndef ASTRO_STEP_H
 #define ASTRO_STEP_H
@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 18
+#define ASTRO_ABI_VERSION 19
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -70,7 +70,7 @@ typedef struct AstroParams {
     int32_t solo;
     int32_t max_planets;   /* create(): 1..max_planets planets */
     int32_t p_pad;         /* planet slots per env, 1..16 (>= max_planets) */
-    int32_t b_cap;         /* live bullets an env may hold, 1..ASTRO_MAX_B_CAP */
+    int32_t b_cap;         /* bullet slots per env, 1..65535 */
     int32_t timeout_tick;  /* first tick k with max_time <= t_k + dt */
     const uint32_t *fire_bits; /* device: bit k = fire on tick k, k < timeout_tick */
     int32_t kernel;        /* ASTRO_KERNEL_AUTO / _LANE / _QUAD / _PAIR (results are identical) */
@@ -81,10 +81,6 @@ typedef struct AstroParams {
     const uint32_t *key_table; /* device, optional: key[397] of MT19937 init_genrand for
                                   every seed < 2^30 (astro_keytable_build); NULL = the
                                   397-step chain at each create (~9 us per lane) */
-    int32_t fire_period;   /* > 0: the schedule is exactly "fire on tick k iff k % fire_period
-                              == fire_phase" for every k < timeout_tick (fire_bits may then
-                              be NULL and is not read); 0: fire_bits decides */
-    int32_t fire_phase;
 } AstroParams;
 
 /* Step kernel variants.  LANE: one lane per env (64 envs per wave64).  QUAD:
@@ -97,15 +93,9 @@ typedef struct AstroParams {
 enum { ASTRO_KERNEL_AUTO = 0, ASTRO_KERNEL_LANE = 1, ASTRO_KERNEL_QUAD = 2, ASTRO_KERNEL_PAIR = 3 };
 #define ASTRO_QUAD_MAX_ENVS 32768
 
-#define ASTRO_MAX_B_CAP 1000
-#define ASTRO_BULLET_GROUP 16
-
 /* Per-env state arrays (device pointers).  hdr packs
  *   hdr[4*i+0] = tick (steps since create, < 2^22)
- *   hdr[4*i+1] = nplanets (5 bits) | flags << 5 (2 bits) | half << 7 |
- *                nbullets << 8 (10 bits) | boff << 18 (14 bits): the env's live
- *                bullets are entries [boff, boff + nbullets) of its bullet
- *                group's region in bullet half `half` (see `bullets`)
+ *   hdr[4*i+1] = nplanets | flags << 8 | nbullets << 16
  *   hdr[4*i+2] = the NEXT game's seed (drawn one game ahead from the stream,
  *                < 2^30) | key_valid << 31, or undrawn << 30 alone: a game's
  *                create leaves the draw to its first step, off the reset path
@@ -119,15 +109,7 @@ typedef struct AstroState {
     void *ships;        /* [nships][n_env][4]  x, y, dx, dy */
     void *ships_b;      /* [nships][n_env]     bearing */
     void *planets;      /* [p_pad][n_env][4]   x, y, dx, dy */
-    void *bullets;      /* [2][n_env * (b_cap + nships)][4]  x, y, dx, dy: two halves.  Envs
-                           16g .. 16g+15 (a bullet group) keep their live bullets in
-                           the group's region of a half, entries from 16g * (b_cap +
-                           nships) on, one env after the other (hdr: half, boff,
-                           nbullets; every env of a group is in the same half).  A step
-                           reads a group from its half and writes it to the other;
-                           astro_reset keeps the half.  Entries between envs' bullets
-                           are unused.  Zeroed hdr words 1 (or astro_stream_init) =
-                           half 0, no bullets. */
+    void *bullets;      /* [n_env][b_cap][4]   x, y, dx, dy (one contiguous row per env) */
     int32_t *hdr;       /* [n_env][4], 16-byte aligned */
     uint32_t *stream;   /* [n_env][4] generate_configs cursor: x_k, x_{k+397}, k, current game's seed
                            (x = the MT19937 word sequence of the env's RandomState, core.py:79) */

@@ -80,8 +80,7 @@ def _gpu_worker(rank, world, port, n_total, ticks, out_dir):
             env.step(ctl[t])
         resets = shard.sum_over_ranks([env.stat_dict()['resets']])[0]
         np.savez(os.path.join(out_dir, 'g%d.npz' % rank), hdr=env.hdr.cpu().numpy(),
-                 ships=env.ships.cpu().numpy(), stream=env.stream.cpu().numpy(),
-                 bullets=env.bullet_rows().cpu().numpy(), resets=resets)
+                 ships=env.ships.cpu().numpy(), stream=env.stream.cpu().numpy(), resets=resets)
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -92,9 +91,7 @@ def test_gpu_ranks_step_their_shards_like_one_run(tmp_path):
     """bench.py's multi-GPU layout end to end on one GPU: 3 gloo ranks (a
     ragged split of 10,000 envs) each step their shard; the concatenated
     states equal a single-process run of all envs bit for bit, and the
-    sum-over-ranks of resets equals the single run's.  (A bullet's place in
-    the packed halves is relative to its 16-env group, which a ragged split
-    moves: headers are compared without the offset field, bullets as rows.)"""
+    sum-over-ranks of resets equals the single run's."""
     import torch
     import bench
     from astro_amd import BatchedEnv
@@ -106,11 +103,7 @@ def test_gpu_ranks_step_their_shards_like_one_run(tmp_path):
     for t in range(ticks):
         env.step(ctl[t])
     parts = [np.load(tmp_path / ('g%d.npz' % r)) for r in range(world)]
-    got, want = np.concatenate([z['hdr'] for z in parts]), env.hdr.cpu().numpy()
-    got[:, 1] &= 0x3ffff   # (hdr word 1 without the bullet offset)
-    want[:, 1] &= 0x3ffff
-    assert np.array_equal(got, want)
-    assert np.array_equal(np.concatenate([z['bullets'] for z in parts]), env.bullet_rows().cpu().numpy())
+    assert np.array_equal(np.concatenate([z['hdr'] for z in parts]), env.hdr.cpu().numpy())
     assert np.array_equal(np.concatenate([z['stream'] for z in parts]), env.stream.cpu().numpy())
     assert np.array_equal(np.concatenate([z['ships'] for z in parts], 1), env.ships.cpu().numpy())
     assert float(parts[0]['resets']) == float(env.stat_dict()['resets']) > 0

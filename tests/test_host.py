@@ -138,41 +138,6 @@ def test_schedule_matches_oracle_and_golden():
         assert sc.t[:50].tolist() == s['t'] and sc.reload[:50].tolist() == s['reload']
 
 
-def test_fire_period_detection():
-    """The kernel's periodic fire arguments (AstroParams.fire_period/phase)
-    are set only when they reproduce the float64 schedule on every tick
-    before the timeout: the presets (default: ticks 14 + 15k; SOLO: never)
-    and reload 0.1 are periodic; reload 0.07 / 0.33 and dt 0.017 drift off
-    any period and keep the bitmask."""
-    from astro_amd.config import SOLO_EASY_CONFIG
-    cases = [(DEFAULT_CONFIG, (15, 14)), (SOLO_CONFIG, (1 << 30, (1 << 30) - 1)),
-             (SOLO_EASY_CONFIG, (1 << 30, (1 << 30) - 1)), (DEFAULT_CONFIG._replace(reload_time=0.1), (5, 4)),
-             (DEFAULT_CONFIG._replace(reload_time=0.07), (0, 0)), (DEFAULT_CONFIG._replace(reload_time=0.33), (0, 0)),
-             (DEFAULT_CONFIG._replace(dt=0.017), (0, 0))]
-    for cfg, want in cases:
-        sch = schedule.build(cfg)
-        got = sch.fire_period()
-        assert got == want, (cfg, got)
-        if got[0]:
-            k = np.arange(sch.timeout_tick)
-            assert np.array_equal((k % got[0]) == got[1], sch.fire)
-
-
-def test_fire_period_float_quotient():
-    """fires_at's tick mod period (astro_kernels.hip) by a float32 quotient and
-    one correction step equals the integer remainder for every tick below
-    2^22 the kernel allows, for small, preset and huge periods (numpy float32
-    is the device's IEEE arithmetic: correctly rounded 1/period, product,
-    truncation)."""
-    ticks = np.arange(1 << 22, dtype=np.int64)
-    for per in (1, 2, 3, 5, 7, 15, 16, 97, 1000, 4095, (1 << 22) - 3, (1 << 22) + 5, 1 << 30):
-        inv = np.float32(1.0) / np.float32(per)
-        qt = (ticks.astype(np.float32) * inv).astype(np.int64)
-        r = ticks - qt * per
-        r = np.where(r < 0, r + per, np.where(r >= per, r - per, r))
-        assert np.array_equal(r, ticks % per), per
-
-
 def test_kernel_constants_match_oracle():
     for cfg in gio.configs().values():
         k = schedule.kernel_constants(cfg)
@@ -235,51 +200,6 @@ def test_kernel_choice_mirrors_header():
     hdr = open(os.path.join(os.path.dirname(__graft_entry__.__file__), 'include', 'astro_step.h')).read()
     n = int(re.search(r'#define ASTRO_QUAD_MAX_ENVS (\d+)', hdr).group(1))
     assert _env.QUAD_MAX_ENVS == n
-    assert _env.MAX_B_CAP == int(re.search(r'#define ASTRO_MAX_B_CAP (\d+)', hdr).group(1))
-    assert _env.BULLET_GROUP == int(re.search(r'#define ASTRO_BULLET_GROUP (\d+)', hdr).group(1))
-
-
-def test_packed_bullet_layout_round_trip():
-    """The packed bullet layout (include/astro_step.h AstroState.bullets):
-    rows -> pack_bullets (load_host's packing, every group in half 0) ->
-    bullet_rows_of (BatchedEnv.bullet_rows' gather) is the identity on live
-    bullets, with ragged groups (a last group of 5 envs); the header fields
-    round-trip; and a group's bullets are contiguous, env after env, in
-    its own region (the worst case, every env full plus its 2 spawn slots,
-    fits the header's 14-bit offsets and the region)."""
-    import torch
-    from astro_amd import env as _env
-    rng = np.random.RandomState(0)
-    N, B, S = 37, 24, 2
-    nb = rng.randint(0, B + 1, N)
-    nb[:3] = [0, B, 1]
-    rows = np.where(np.arange(B)[None, :, None] < nb[:, None, None], rng.uniform(-2, 2, (N, B, 4)), 0.0)
-    packed, boff = _env.pack_bullets(rows, nb, S)
-    assert packed.shape == (2, N * (B + S), 4) and not packed[1].any()
-    for g in range(0, N, 16):   # a group's bullets: one block from its region's start
-        m = slice(g, min(N, g + 16))
-        assert boff[g] == 0 and (np.diff(boff[m]) == nb[m][:-1]).all()
-        region = packed[0, g * (B + S):g * (B + S) + int(nb[m].sum())]
-        assert np.array_equal(region, np.concatenate([rows[i, :nb[i]] for i in range(g, min(N, g + 16))]))
-    flags = rng.randint(0, 4, N)
-    w1 = _env.hdr_word1(rng.randint(1, 17, N), flags, 0, nb, boff)
-    got = _env.bullet_rows_of(torch.from_numpy(packed), torch.from_numpy(w1.view(np.int32)), B, S)
-    assert np.array_equal(got.numpy(), rows)
-    t = torch.from_numpy(w1.view(np.int32))
-    assert ((t >> 8) & 0x3ff).numpy().tolist() == nb.tolist() and ((t >> 5) & 3).numpy().tolist() == flags.tolist()
-    # the other half, offsets past 2^13 (the word's sign bit): same gather
-    M = _env.MAX_B_CAP
-    worst = 15 * (M + S)   # env 15's offset when envs 0..14 hold M bullets and 2 spawn slots each
-    assert worst + M <= 16 * (M + S) and worst < 1 << 14
-    nbw = np.zeros(16, np.int64)
-    nbw[15] = 2
-    offs = np.zeros(16, np.int64)
-    offs[15] = worst
-    w1 = _env.hdr_word1(np.full(16, 3), 0, 1, nbw, offs)
-    big = torch.zeros(2, 16 * (M + S), 4)
-    big[1, worst:worst + 2] = torch.tensor([[1., 2., 3., 4.], [5., 6., 7., 8.]])
-    r = _env.bullet_rows_of(big, torch.from_numpy(w1.view(np.int32)), M, S)
-    assert r[15, :2].tolist() == [[1., 2., 3., 4.], [5., 6., 7., 8.]] and not r[15, 2:].any() and not r[:15].any()
 
 
 def test_filtered_stream_oracle_matches_numpy():
