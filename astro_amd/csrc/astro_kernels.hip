@@ -70,9 +70,9 @@ template <> struct Store<double> { using V = D4; };
 
 
 // A state store of the step: nontemporal (the next launch reads it from
-// HBM anyway; streamed, the stores leave L2 to the launch's loads; A/B in
-// profiles/round4/ab_nt_stores.jsonl).  A/B build -DASTRO_TEMPORAL_STORES:
-// plain stores
+// HBM anyway; streamed, the stores leave L2 to the launch's loads: c3 11.88
+// -> 11.77 us, c5 32.03 -> 31.72 us, c2 even, profiles/round4/ab_nt_stores.jsonl).
+// A/B build -DASTRO_TEMPORAL_STORES: plain stores
 template <typename X>
 __device__ __forceinline__ void st_out(X *p, const X &v) {
 #ifndef ASTRO_TEMPORAL_STORES
@@ -2970,8 +2970,9 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 
 // Waves per SIMD the one-tick instances without helpers are built for:
 // 8 planet slots: 3 (141 VGPRs, no spills; at 4: 128 VGPRs, 41 spilled, c5
-// 34.3 -> 31.1 us); 4 slots: 3 (at 4: no gain, c3 at 1M envs 114.0 vs
-// 114.3 us, profiles/round4/ab_packed_bullets_v8v9.jsonl).
+// 34.3 -> 31.1 us); 4 slots: 4 (127 VGPRs with one bullet round at a time,
+// no spills; c3 at 1M envs 131.8 us at 3, 119.2 at 4,
+// profiles/round4/ab_1m_waves.jsonl).
 // The K-tick (rollout) instances: 4 planet slots at 3 waves per SIMD (168
 // VGPRs; at 2 the 1M-env rollouts ran 110 vs 91 us per tick,
 // profiles/round4/ab_packed_bullets_v1.jsonl), 8 slots and the ScriptBot
@@ -2981,7 +2982,7 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 #define ASTRO_P8_WAVES 3
 #endif
 #ifndef ASTRO_P4_WAVES
-#define ASTRO_P4_WAVES 3
+#define ASTRO_P4_WAVES 4
 #endif
 #ifndef ASTRO_M4_WAVES
 #define ASTRO_M4_WAVES 3
