@@ -2285,8 +2285,9 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           // latency sets, with helper waves or K ticks); with 8 the registers
           // of two rounds spill (measured: c5 30.8 -> 34.3 us), and the
           // one-tick instances without helpers (millions of envs, HBM-bound)
-          // keep the registers for occupancy instead (c3 at 1M envs 128.3 ->
-          // 114.0 us, profiles/round4/ab_packed_bullets_v8v9.jsonl): one at a time
+          // keep the registers for occupancy instead (4 waves per SIMD with
+          // no spills: c3 at 1M envs 127.5 -> 119.2 us,
+          // profiles/round4/ab_1m_waves.jsonl): one at a time
           constexpr int NR2 = PMAX <= 4 ? NRW : 1;
           if (nr >= 3) {
               bws[2] = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
