@@ -30,7 +30,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from astro_amd import BatchedEnv, DEFAULT_CONFIG  # noqa: E402
-from astro_amd import _lib  # noqa: E402
 from astro_amd import shard as _shard  # noqa: E402
 
 METRIC = 'env-steps/sec (batched lockstep) at 1/2/4/8 MI355X vs CPU core.step'
@@ -313,9 +312,6 @@ def main():
                     help="how the timed region replays a captured graph: hipGraphLaunch on its executable "
                          "graph directly (default: no per-replay wrapper; 20-step wall 14.75 -> 13.92 us median, "
                          "profiles/round3s2/ab_replay.jsonl), or torch's CUDAGraph.replay()")
-    ap.add_argument('--s0', default='device', choices=['device', 'host'],
-                    help="the region's starting counters: a device snapshot read after the region, or "
-                         "stat_dict() before it (a host round trip between the warm replays and the clock)")
     ap.add_argument('--end-poll', default='event', choices=['event', 'stream'],
                     help="how the host sees the region's end before its synchronize: busy-poll an event "
                          "recorded behind the launches, or busy-poll the stream itself (no event in the region)")
@@ -439,16 +435,8 @@ def main():
             ev_w.record(stream)
             while not ev_w.query():
                 pass
-    if args.s0 == 'host':
-        barrier()
-        s0 = env.stat_dict()
-    else:
-        # the region's starting counters as a device snapshot, read after the
-        # region: no host round trip (a sum kernel, a copy, the error word)
-        # between the warm replays and the clock, so the GPU idles as little
-        # as the synchronize allows (profiles/round4/ab_s0_20steps.jsonl)
-        env.check_errors()
-        s0_dev = env.stats.sum(0)
+    barrier()
+    s0 = env.stat_dict()
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     poll_event = args.end_poll == 'event'
@@ -473,8 +461,6 @@ def main():
     # faults of the timed region (read before stat_dict, which raises on them)
     dev_err = env.device_errors(clear=False)
     barrier()
-    if args.s0 != 'host':
-        s0 = dict(zip(_lib.STAT_NAMES, s0_dev.cpu().tolist()))
     s1 = env.stat_dict() if not dev_err else dict(s0)
     gpu_ms_stream = ev0.elapsed_time(ev1) / args.steps if poll_event else None
     gpu_ms_graph = None

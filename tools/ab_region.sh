@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved runs of the driver's c3 command (--steps 20 --warmup 5) under
 # two bench settings, one bench process each (the region is what differs):
-#   A="--s0 host" B="--s0 device" [C=... VARS="A B C"] N=4 bash tools/ab_region.sh
+#   A="--warm-ms 20" B="--warm-ms 100" [C=... VARS="A B C"] N=4 bash tools/ab_region.sh
 # -> gpurun_out/ab_region.jsonl, one line per run with its setting in "ab".
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
