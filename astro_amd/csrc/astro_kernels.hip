@@ -1351,6 +1351,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
 #ifdef ASTRO_STAMPS
     if (stats && (threadIdx.x & 63) == 0) {
         unsigned long long *row = stats + size_t(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * NSTAMP;
+#pragma unroll
         for (int k = 0; k < NSTAMP; ++k) row[k] = stamp_[k];
     }
     return;
@@ -3004,7 +3005,12 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
     if (stats && (threadIdx.x & 63) == 0) {   // a helper wave: slots 20-22 of its step wave's row
         const bool hw = int(threadIdx.x) >= (64 * WPG);
         unsigned long long *row = stats + size_t(blockIdx.x * WPG + (threadIdx.x / 64) % WPG) * NSTAMP;
-        for (int k = hw ? 20 : 0; k < (hw ? 23 : 20); ++k) row[k] = stamp_[k];
+        // (constant indices only: a loop over a runtime range put the stamp
+        // array in scratch, and its stores then sat in the same vmcnt queue
+        // as the wave's first loads -- the header wait measured them too)
+#pragma unroll
+        for (int k = 0; k < 23; ++k)
+            if (hw == (k >= 20)) row[k] = stamp_[k];
     }
 #else
     // ---- the launch's ticks: each wave steps its 16 envs on its own, no
