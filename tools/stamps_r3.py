@@ -30,6 +30,9 @@ def main():
     ap.add_argument('--lib', default='libastro_hip_stamps')
     ap.add_argument('--ticks', type=int, default=20)
     ap.add_argument('--warm', type=int, default=300)
+    ap.add_argument('--b2b', action='store_true',
+                    help='the measured launches back to back (one stats buffer each, one sync at the end): '
+                         'adds the gap between a launch\'s last wave and the next launch\'s first')
     a = ap.parse_args()
     _lib._lib = None
     _lib.load(os.path.join(ROOT, 'astro_amd', a.lib + '.so'))
@@ -46,11 +49,20 @@ def main():
     for t in range(5):
         env.launch(ctl[t].data_ptr(), stats=False)
     rows = []
-    for t in range(a.ticks):
-        env.stats.zero_()
-        env.launch(ctl[5 + t].data_ptr(), stats=True)
+    if a.b2b:
+        bufs = [torch.zeros(nw, NSTAMP, dtype=torch.int64, device='cuda') for _ in range(a.ticks)]
         torch.cuda.synchronize()
-        rows.append(env.stats.cpu().numpy().astype(np.int64))
+        for t in range(a.ticks):
+            env.stats = bufs[t]
+            env.launch(ctl[5 + t].data_ptr(), stats=True)
+        torch.cuda.synchronize()
+        rows = [b.cpu().numpy().astype(np.int64) for b in bufs]
+    else:
+        for t in range(a.ticks):
+            env.stats.zero_()
+            env.launch(ctl[5 + t].data_ptr(), stats=True)
+            torch.cuda.synchronize()
+            rows.append(env.stats.cpu().numpy().astype(np.int64))
     S = np.concatenate(rows, 0)
     tot = S[:, 11] - S[:, 0]
     out = dict(workload=a.workload, n=n, kernel=env.step_kernel, waves=nw, wave_cycles_mean=float(tot.mean()))
@@ -68,6 +80,22 @@ def main():
     out['wave_start_us_mean'] = float(np.concatenate(st).mean())
     out['wave_end_us_mean'] = float(np.concatenate(en).mean())
     out['launch_last_wave_end_us'] = float(np.mean([e.max() for e in en]))
+    # every launch's first wave start and last wave end (step or helper) on
+    # the 100 MHz real-time clock: with --b2b the time between launches
+    first = [int(S[t * nw:(t + 1) * nw, 12].min()) for t in range(a.ticks)]
+    last = []
+    for t in range(a.ticks):
+        R = S[t * nw:(t + 1) * nw]
+        e = int(R[:, 13].max())
+        if (R[:, 21] > 0).any():
+            e = max(e, int(R[R[:, 21] > 0, 21].max()))
+        last.append(e)
+    if a.b2b:
+        span = [(last[t] - first[t]) / 100.0 for t in range(a.ticks)]
+        gap = [(first[t + 1] - last[t]) / 100.0 for t in range(a.ticks - 1)]
+        per = [(first[t + 1] - first[t]) / 100.0 for t in range(a.ticks - 1)]
+        out['b2b'] = dict(span_us_mean=float(np.mean(span)), gap_us_mean=float(np.mean(gap)),
+                          gap_us_min=float(np.min(gap)), period_us_mean=float(np.mean(per)))
     if (S[:, 21] > 0).any():
         he = []
         for t in range(a.ticks):
