@@ -19,10 +19,11 @@ def shard(n_total, rank, world):
 
 def max_over_ranks(value, device=None):
     """Max of a float over all ranks of the default process group (or the
-    value itself when not distributed)."""
+    value itself when no group is initialised; a one-rank group still runs
+    the all_reduce, so the collective path is the same at every size)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -33,7 +34,7 @@ def sum_over_ranks(values, device=None):
     """Element-wise sum of a list of numbers over all ranks."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [float(v) for v in values]
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)

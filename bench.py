@@ -261,7 +261,8 @@ def stub_rank(args, world, rank):
         print(json.dumps(out), flush=True)
 
 
-PROFILE_ROUNDS = ('round4', 'round3', 'round2')
+PROFILE_ROUNDS = ('round5', 'round4', 'round3', 'round2')
+ROLLOUT_LAUNCHES = 10   # the rollout line's launches at least
 
 
 def profile_file(name):
@@ -334,7 +335,11 @@ def main():
     torch.cuda.set_device(dev)
     backend = os.environ.get('ASTRO_DIST_BACKEND', 'nccl')
     red_dev = dev if backend == 'nccl' else None
-    if world > 1:
+    # the process group: every multi-rank run, and a single rank when
+    # ASTRO_DIST_INIT=1 (the RCCL initialisation, barrier and device-tensor
+    # reductions of the multi-GPU path, exercised on one GPU)
+    dist_on = world > 1 or os.environ.get('ASTRO_DIST_INIT', '') == '1'
+    if dist_on:
         import torch.distributed as dist
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
@@ -358,7 +363,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if dist_on:
             import torch.distributed as dist
             dist.barrier()
 
@@ -516,7 +521,9 @@ def main():
     extras = {}
     if args.rollout > 0:
         K = args.rollout
-        reps = max(1, args.steps // K)
+        # a fixed number of launches whatever --steps is (the driver's 20-step
+        # run and a 1,000-step run time the same rollout region)
+        reps = max(ROLLOUT_LAUNCHES, args.steps // K)
         base = ticks + args.calib
         env.rollout(K, 'random', tick0=base, stats=False)
         barrier()
@@ -653,6 +660,9 @@ def main():
                                        len(graphs), args.graph,
                                        'hipGraphLaunch' if args.replay == 'raw' else 'torch CUDAGraph.replay'))
                 if graphs else 'no graph'),
+            dist=dict(initialized=dist_on, backend=backend if dist_on else None, world=world,
+                      reductions='device tensors (RCCL all_reduce)' if dist_on and red_dev is not None
+                      else ('host tensors (gloo)' if dist_on else 'none (one rank)')),
             burn_in_ticks=args.burn_in, settle_launches=settle, warm_ms=args.warm_ms,
             device_errors=int(tot[7]),
             stats=dict(mean_live_bullets=mlb,
@@ -668,7 +678,7 @@ def main():
     # rank 0's host-side lines run after every rank has left the GPU region
     # (the last collective above): the CPU baseline of the same workload, on
     # this rank's CPU share, for any number of ranks
-    if world > 1:
+    if dist_on:
         import torch.distributed as dist
         dist.destroy_process_group()
     if rank == 0:

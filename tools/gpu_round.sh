@@ -18,9 +18,10 @@ run() {
 }
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ;;
+    driver) run driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -f csv -- \
                 python bench.py --steps 300 --no-cpu ;;
   esac
