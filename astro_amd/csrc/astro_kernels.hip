@@ -579,37 +579,37 @@ __device__ __forceinline__ CreateDraws<S> create_draws(const CreateWords<S> &cw)
 }
 
 // ---------------------------------------------------------------------------
+// Where create() puts a new game.  GlobalSink: the state arrays in HBM (every
+// launch but the resident rollout); the resident rollout's sinks put it in
+// LDS (a reset pass) or in the env's own registers (the serial create).
+template <typename T>
+struct GlobalSink {
+    using V = typename Store<T>::V;
+    const AstroState &st;
+    __device__ void ship(int s, int ie, const V &v, T b) const {
+        reinterpret_cast<V *>(st.ships)[size_t(s) * size_t(st.n_env) + ie] = v;
+        reinterpret_cast<T *>(st.ships_b)[size_t(s) * size_t(st.n_env) + ie] = b;
+    }
+    // planet slot j (the caller's m-th slot of its part)
+    __device__ void planet(int j, int m, int ie, const V &v) const {
+        (void)m;
+        reinterpret_cast<V *>(st.planets)[size_t(j) * size_t(st.n_env) + ie] = v;
+    }
+    __device__ void header(int ie, const int4 &h) const { reinterpret_cast<int4 *>(st.hdr)[ie] = h; }
+    __device__ GlobalSink for_row(int) const { return *this; }   // (a reset pass's row r)
+};
+
+// ---------------------------------------------------------------------------
 // create() (core.py:86-135) for env i from `seed`; writes the env's slots.
 // NPART lanes may share one env: each runs the (cheap, serial) random draws
 // and writes ships s and planets j with s, j = part mod NPART, so the
 // trigonometry of the planets runs in parallel.
 
-template <typename T, int S, int PMAX, int NPART = 1>
-__device__ int create_env(const AstroParams &p, const AstroState &st, int i, const CreateDraws<S> &d,
+template <typename T, int S, int PMAX, int NPART = 1, class Sink = GlobalSink<T>>
+__device__ int create_env(const AstroParams &p, const Sink &sink, int i, const CreateDraws<S> &d,
                           int &flags_out, int part = 0) {
     using V = typename Store<T>::V;
-    const size_t N = size_t(st.n_env);
-    V *ships = reinterpret_cast<V *>(st.ships);
-    T *ships_b = reinterpret_cast<T *>(st.ships_b);
-    V *planets = reinterpret_cast<V *>(st.planets);
 
-#ifdef ASTRO_STUB_CREATE   // timing experiment only: a fixed 3-planet game, no RNG/trig
-    {
-        V v;
-        v.z = v.w = T(0);
-        v.x = T(0.9f); v.y = T(-0.9f); ships[i] = v; ships_b[i] = T(1.0f);
-        if (S == 2) { v.x = T(-0.2f); v.y = T(0.1f); ships[N + i] = v; ships_b[N + i] = T(2.0f); }
-        const float px[3] = {0.5f, -0.25f, -0.25f}, py[3] = {0.0f, 0.433f, -0.433f};
-        for (int j = 0; j < 3 && j < PMAX; ++j) {
-            V w;
-            w.x = T(px[j]); w.y = T(py[j]); w.z = T(-0.1f * py[j]); w.w = T(0.1f * px[j]);
-            planets[size_t(j) * N + i] = w;
-        }
-        flags_out = 0;
-        (void)d;
-        return PMAX < 3 ? PMAX : 3;
-    }
-#endif
     int n = d.n;
     // outer = outer_ship_position * sign(rand(2).astype(float32) - 0.5)
     const float u0 = float(d.u_out[0]) - 0.5f;
@@ -646,15 +646,12 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, con
         v.y = T(shy[s]);
         v.z = T(0);
         v.w = T(0);
-        if (s % NPART == part) {
-            ships[size_t(s) * N + i] = v;
-            ships_b[size_t(s) * N + i] = T(b);
-        }
+        if (s % NPART == part) sink.ship(s, i, v, T(b));
     }
     if (n == 1) {
         V v;
         v.x = v.y = v.z = v.w = T(0);
-        if (part == 0) planets[i] = v;
+        if (part == 0) sink.planet(0, 0, i, v);
     } else {
         const double base = TWO_PI * d.u_base;
         const double stp = TWO_PI / double(n);
@@ -674,7 +671,7 @@ __device__ int create_env(const AstroParams &p, const AstroState &st, int i, con
             v.y = T(p.planet_orbit * pc);
             v.z = T(amp * double(vs));
             v.w = T(amp * double(vc));
-            planets[size_t(j) * N + i] = v;
+            sink.planet(j, m, i, v);
         }
     }
     if (n > PMAX) n = PMAX;
@@ -732,15 +729,15 @@ __device__ __forceinline__ NextGame<S> next_game(const AstroParams &p, uint32_t 
 
 // Start env i's next game from its NextGame: create (the float half), then
 // the stream record and header (part 0).
-template <typename T, int S, int PMAX, int NPART = 1>
+template <typename T, int S, int PMAX, int NPART = 1, class Sink = GlobalSink<T>>
 __device__ __forceinline__ void restart_env(const AstroParams &p, const AstroState &st, int i,
-                                            const NextGame<S> &ng, int part = 0) {
+                                            const NextGame<S> &ng, int part, const Sink &sink) {
     int cf = 0;
-    const int n = create_env<T, S, PMAX, NPART>(p, st, i, create_draws<S>(ng.words), cf, part);
+    const int n = create_env<T, S, PMAX, NPART, Sink>(p, sink, i, create_draws<S>(ng.words), cf, part);
     if (part != 0) return;
     reinterpret_cast<uint4 *>(st.stream)[i] = make_uint4(ng.ca, ng.cb, ng.ci, ng.seed);
     const int flags = (ng.exhausted || cf) ? 2 : 0;
-    reinterpret_cast<int4 *>(st.hdr)[i] = make_int4(0, n | (flags << 8), int(UNDRAWN), 0);
+    sink.header(i, make_int4(0, n | (flags << 8), int(UNDRAWN), 0));
 }
 
 // The pending seed at the end of a step (the lane holding the env's header):
@@ -1341,7 +1338,7 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                 const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
                 const NextGame<S> ng = next_game<S>(p, pend_seed, pend_key, key_valid || p.key_table, undrawn, c,
                                                     stream_ring_of(st, i));
-                restart_env<T, S, PMAX>(p, st, i, ng);
+                restart_env<T, S, PMAX>(p, st, i, ng, 0, GlobalSink<T>{st});
                 f_reset = true;
             }
             STAMP(10);
@@ -1561,10 +1558,10 @@ __device__ __forceinline__ uint32_t bw_tag(int e, int np, bool t0) {
 // those in the window, lane q a contiguous run of ceil(nb / LPE) slots (the
 // word of slot k + 1 is the word of slot k plus 1 << 5: an add and an LDS
 // store per slot; the last slot's flag is OR-ed in after the loop).
-template <int LPE>
+template <int LPE, int QWN = QWIN>
 __device__ __forceinline__ void index_window(uint32_t *s_index, int w0, int off, int nb, int q, uint32_t tag) {
     const int h = (nb + LPE - 1) / LPE;
-    const int k0 = max(q * h, w0 - off), k1 = min(min(nb, (q + 1) * h), w0 + QWIN - off);
+    const int k0 = max(q * h, w0 - off), k1 = min(min(nb, (q + 1) * h), w0 + QWN - off);
     uint32_t w = tag | (uint32_t(k0) << 5);
     uint32_t *dst = s_index + (off + k0 - w0);
     for (int k = k0; k < k1; ++k, w += 1u << 5) *dst++ = w;
@@ -1624,12 +1621,11 @@ __device__ __forceinline__ typename Store<T>::V create_planet(const AstroParams 
 // and the results move by shuffles; lane s < S writes ship s, lane j < n
 // planet j (same arithmetic as create_env, bit for bit).  All lanes of the
 // row must be active; `write` gates the stores.
-template <typename T, int S, int PMAX>
-__device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroState &st, int ie,
+template <typename T, int S, int PMAX, class Sink>
+__device__ __forceinline__ int create_env_row(const AstroParams &p, const Sink &sink, int ie,
                                               const CreateDraws<S> &d, int u, int row0, bool write) {
     static_assert(2 * PMAX + 1 <= 16, "one angle per lane of a 16-lane row");
     using V = typename Store<T>::V;
-    const size_t N = size_t(st.n_env);
     int n = d.n;
     const double stp = TWO_PI / double(n);
     const double base = TWO_PI * d.u_base;
@@ -1646,14 +1642,11 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
     // ships (core.py:93-109): lane u < S writes ship u
     T b;
     const V sv = create_ship<T, S>(p, d, S == 2 && u == 1, is, ic, b);
-    if (write && u < S) {
-        reinterpret_cast<V *>(st.ships)[size_t(u) * N + ie] = sv;
-        reinterpret_cast<T *>(st.ships_b)[size_t(u) * N + ie] = b;
-    }
+    if (write && u < S) sink.ship(u, ie, sv, b);
     // planets (core.py:111-121): lane j < n writes planet j
     if (write && u < PMAX) {
         const V v = create_planet<T>(p, n, sn, cs, vs, vc);
-        if (u < n) reinterpret_cast<V *>(st.planets)[size_t(u) * N + ie] = v;
+        if (u < n) sink.planet(u, 0, ie, v);
     }
     if (n > PMAX) n = PMAX;
     return n;
@@ -1672,11 +1665,11 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const AstroS
 // create, and so is one whose game ended at its first step (its seed still
 // UNDRAWN).  The stream cursor is left alone: the next game's seed is drawn
 // by the env's first step.  Returns the leaders not yet served.
-template <typename T, int S, int PMAX, int LPE, bool PRE = false>
+template <typename T, int S, int PMAX, int LPE, bool PRE = false, class Sink = GlobalSink<T>>
 __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const AstroState &st, uint64_t todo,
                                                     int lane, int i, uint32_t pend_seed, uint32_t pend_key,
                                                     bool have_key, bool undrawn, uint32_t (*s_chain)[2][13 + 2 * S],
-                                                    int *s_serial STAMP_ARG,
+                                                    int *s_serial, const Sink &sink_all STAMP_ARG,
                                                     const uint32_t (*pre)[2][13 + 2 * S] = nullptr) {
     constexpr int NW = 12 + 2 * S;   // outputs create() draws, randint accepting its first word
     int leader[4];
@@ -1757,17 +1750,18 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     d.exhausted = false;   // NW outputs, far below the 227 the lazy generator covers
     STAMP(17);
 
+    const Sink sink = sink_all.for_row(row);   // where row `row`'s game goes
     int n, cf = 0;
     if constexpr (2 * PMAX + 1 <= 16) {
-        n = create_env_row<T, S, PMAX>(p, st, ie, d, u, row0, on && fast);
+        n = create_env_row<T, S, PMAX>(p, sink, ie, d, u, row0, on && fast);
     } else {
-        if (on && fast) n = create_env<T, S, PMAX, 16>(p, st, ie, d, cf, u);
+        if (on && fast) n = create_env<T, S, PMAX, 16, Sink>(p, sink, ie, d, cf, u);
     }
     STAMP(18);
     if (on && fast) {
         if (u == 0) {   // the stream record's game seed and the header, as restart_env
             st.stream[4 * size_t(ie) + 3] = seed;
-            reinterpret_cast<int4 *>(st.hdr)[ie] = make_int4(0, n | (cf ? 2 << 8 : 0), int(UNDRAWN), 0);
+            sink.header(ie, make_int4(0, n | (cf ? 2 << 8 : 0), int(UNDRAWN), 0));
         }
     }
     if (on && !fast && u == 0) s_serial[L / LPE] = 1;
@@ -2048,12 +2042,71 @@ struct BulletsIn {
     typename Store<T>::V cur0, cur1;
 };
 
-template <typename T, int LPE>
-__device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroState &st, size_t BC, int lane, int e, int q, int base,
-                                                      int nb, int np, bool t0, uint32_t *s_index, int *s_kept,
-                                                      int *s_hit, int *s_serial) {
+// Where the dense pass finds the wave's bullet rows and, for its rare exact
+// tests, the old bodies at full precision.  BulletsGlobal: the state's rows
+// in HBM ([n_env][b_cap], env base + e); BulletsLds: the resident rollout's
+// rows in LDS ([QENV][RES_BCAP] per wave, float32 state) with the old bodies
+// from the pass's own float32 copies (exact: the state is float32).
+template <typename T>
+struct BulletsGlobal {
     using V = typename Store<T>::V;
-    const V *bullets = reinterpret_cast<const V *>(st.bullets);
+    V *rows;
+    const V *ships, *planets;
+    size_t BC, NN;
+    int base;
+    __device__ V load(int e, int slot) const { return rows[size_t(base + e) * BC + slot]; }
+    __device__ void store(int e, int slot, const V &v) const { st_out(&rows[size_t(base + e) * BC + slot], v); }
+    __device__ double2 planet(int e, int j) const {
+        const V v = planets[size_t(j) * NN + size_t(base + e)];
+        return make_double2(double(v.x), double(v.y));
+    }
+    __device__ double2 ship(int e, int s) const {
+        const V v = ships[size_t(s) * NN + size_t(base + e)];
+        return make_double2(double(v.x), double(v.y));
+    }
+};
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) v4f lds_f4;
+typedef __attribute__((address_space(3))) v2f lds_f2;
+__device__ __forceinline__ lds_f4 *lds_ptr(const void *p) {   // a generic LDS address's low half is its offset
+    return (lds_f4 *)size_t(uint32_t(reinterpret_cast<uintptr_t>(p)));
+}
+
+constexpr int RES_BCAP = 32;   // bullet slots per env the resident rollout keeps in LDS
+
+template <int S, int NBOD2>
+struct BulletsLds {
+    using V = F4;
+    lds_f4 *rows;     // [QENV][RES_BCAP]
+    lds_f4 *body;     // [QENV][NBOD2]: (x, y) of ships then planets, float32 = the state's values
+    __device__ V load(int e, int slot) const {
+        const v4f v = rows[e * RES_BCAP + slot];
+        return F4{v.x, v.y, v.z, v.w};
+    }
+    __device__ void store(int e, int slot, const V &v) const {
+        v4f w;
+        w.x = v.x;
+        w.y = v.y;
+        w.z = v.z;
+        w.w = v.w;
+        rows[e * RES_BCAP + slot] = w;
+    }
+    __device__ double2 planet(int e, int j) const {
+        const v2f v = reinterpret_cast<lds_f2 *>(body + e * NBOD2)[S + j];
+        return make_double2(double(v.x), double(v.y));
+    }
+    __device__ double2 ship(int e, int s) const {
+        const v2f v = reinterpret_cast<lds_f2 *>(body + e * NBOD2)[s];
+        return make_double2(double(v.x), double(v.y));
+    }
+};
+
+template <typename T, int LPE, int QWN = QWIN, class BM>
+__device__ __forceinline__ BulletsIn<T> bullets_begin(const BM &bm, int lane, int e, int q, int nb, int np, bool t0,
+                                                      uint32_t *s_index, int *s_kept, int *s_hit, int *s_serial) {
+    using V = typename Store<T>::V;
     BulletsIn<T> b;
     const int incl = wave_incl_scan(q == 0 ? nb : 0, lane);
     b.off = incl - nb;
@@ -2073,21 +2126,21 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const AstroState &st, size
         b.cur0 = b.cur1 = V{};
         return b;
     }
-    index_window<LPE>(s_index, 0, b.off, nb, q, b.tag);
+    index_window<LPE, QWN>(s_index, 0, b.off, nb, q, b.tag);
     wave_sync();
     b.bw0 = lane < b.total ? s_index[lane] : 0u;
-    b.bw1 = lane + 64 < min(b.total, QWIN) ? s_index[lane + 64] : 0u;
-    b.cur0 = bullets[size_t(base + bw_env(b.bw0)) * BC + bw_slot(b.bw0)];
-    b.cur1 = bullets[size_t(base + bw_env(b.bw1)) * BC + bw_slot(b.bw1)];
+    b.bw1 = lane + 64 < min(b.total, QWN) ? s_index[lane + 64] : 0u;
+    b.cur0 = bm.load(bw_env(b.bw0), bw_slot(b.bw0));
+    b.cur1 = bm.load(bw_env(b.bw1), bw_slot(b.bw1));
     return b;
 }
 
 // sxf/syf: both ships' old positions (float32); mpxf/mpyf: the lane's own
 // planet slots q + LPE m (float32, slots past the env's planets parked at
 // -FAR_POS).  Ends with the wave's LDS results readable (wave_sync).
-template <typename T, int S, int PMAX, int LPE, int NRW = 2>
-__device__ __forceinline__ void bullets_rounds(const AstroParams &p, const AstroState &st, const BulletsIn<T> &b,
-                                               int lane, int e, int q, int base, int nb, const float (&sxf)[S],
+template <typename T, int S, int PMAX, int LPE, int NRW = 2, int QWN = QWIN, class BM>
+__device__ __forceinline__ void bullets_rounds(const AstroParams &p, const BM &bm, const BulletsIn<T> &b,
+                                               int lane, int e, int q, int nb, const float (&sxf)[S],
                                                const float (&syf)[S], const float (&mpxf)[PMAX / LPE],
                                                const float (&mpyf)[PMAX / LPE],
                                                float4 (*s_body)[(S + PMAX + 1) / 2], uint32_t *s_index,
@@ -2095,11 +2148,6 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
     using V = typename Store<T>::V;
     constexpr int PPL = PMAX / LPE;
     constexpr int NBOD2 = (S + PMAX + 1) / 2;
-    const size_t NN = size_t(st.n_env);
-    const size_t BC = size_t(p.b_cap);
-    const V *ships = reinterpret_cast<const V *>(st.ships);
-    const V *planets = reinterpret_cast<const V *>(st.planets);
-    V *bullets = reinterpret_cast<V *>(st.bullets);
     const int total = b.total, off = b.off;
     const uint32_t tag = b.tag;
     uint32_t bw0 = b.bw0, bw1 = b.bw1;
@@ -2130,16 +2178,16 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
         const double dt = p.dt;
         int kept_before = 0;   // kept bullets of the wave in earlier rounds
         int carry = 0;         // kept_before at the start of the env spanning into the next round
-        for (int w0 = 0; w0 < total; w0 += QWIN) {   // uniform; one window unless > 64 bullets/env
-          const int wend = min(total, w0 + QWIN);
+        for (int w0 = 0; w0 < total; w0 += QWN) {   // uniform; one window unless > QWN / 32 bullets/env
+          const int wend = min(total, w0 + QWN);
           if (w0 > 0) {
               wave_sync();   // the previous window is read
-              index_window<LPE>(s_index, w0, off, nb, q, tag);
+              index_window<LPE, QWN>(s_index, w0, off, nb, q, tag);
               wave_sync();
               bw0 = w0 + lane < wend ? s_index[lane] : 0u;
               bw1 = w0 + 64 + lane < wend ? s_index[64 + lane] : 0u;
-              cur0 = bullets[size_t(base + bw_env(bw0)) * BC + bw_slot(bw0)];
-              cur1 = bullets[size_t(base + bw_env(bw1)) * BC + bw_slot(bw1)];
+              cur0 = bm.load(bw_env(bw0), bw_slot(bw0));
+              cur1 = bm.load(bw_env(bw1), bw_slot(bw1));
           }
           // one round: lane g takes live bullet r0 + g (index word bw, data cur)
           // NR rounds at once, lane g of round r taking live bullet r0 + 64 r + g
@@ -2190,21 +2238,20 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
 #pragma unroll
                   for (int r = 0; r < NR; ++r) {
                       if (amb[r]) {
-                          const size_t ie = size_t(base + be[r]);
                           const int bnp = bw_np(bws[r]);
                           const double x = double(curs[r].x), y = double(curs[r].y);
                           bool bh64 = false;
 #pragma unroll
                           for (int j = 0; j < PMAX; ++j) {
                               if (j < bnp) {
-                                  const V pj = planets[size_t(j) * NN + ie];
-                                  bh64 |= closer_exact(x, y, double(pj.x), double(pj.y), gp, bt0[r]);
+                                  const double2 pj = bm.planet(be[r], j);
+                                  bh64 |= closer_exact(x, y, pj.x, pj.y, gp, bt0[r]);
                               }
                           }
 #pragma unroll
                           for (int s = 0; s < S; ++s) {
-                              const V sj = ships[size_t(s) * NN + ie];
-                              hs[r][s] = closer_exact(x, y, double(sj.x), double(sj.y), gs, bt0[r]);
+                              const double2 sj = bm.ship(be[r], s);
+                              hs[r][s] = closer_exact(x, y, sj.x, sj.y, gs, bt0[r]);
                           }
                           bh[r] = bh64;
                       }
@@ -2268,7 +2315,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
                   const int first = lane - bw_slot(bws[r]);   // lane of the env's slot 0 (< 0: an earlier round)
                   const int k0 = first >= 0 ? kept_before + __popcll(kb & ((1ull << (first & 63)) - 1)) : carry;
                   const int pos = kg - k0;
-                  if (kp) st_out(&bullets[size_t(base + be[r]) * BC + pos], out[r]);
+                  if (kp) bm.store(be[r], pos, out[r]);
                   if (valid[r] && bw_last(bws[r])) s_kept[be[r]] = pos + int(kp);
                   carry = __builtin_amdgcn_readlane(k0, 63);
                   kept_before += __popcll(kb);
@@ -2292,7 +2339,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           constexpr int NR2 = PMAX <= 4 ? NRW : 1;
           if (nr >= 3) {
               bws[2] = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
-              curs[2] = bullets[size_t(base + bw_env(bws[2])) * BC + bw_slot(bws[2])];
+              curs[2] = bm.load(bw_env(bws[2]), bw_slot(bws[2]));
           }
           if (nr >= 2) {
               rounds(std::integral_constant<int, NR2>(), w0, bws, curs);
@@ -2304,7 +2351,7 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const Astro
           if (nr >= 3) rounds(std::integral_constant<int, 1>(), w0 + 128, bws + 2, curs + 2);
           for (int r0 = w0 + 192; r0 < wend; r0 += 64) {   // uniform; rare
               const uint32_t bw = r0 + lane < wend ? s_index[r0 + lane - w0] : 0u;
-              const V cur = bullets[size_t(base + bw_env(bw)) * BC + bw_slot(bw)];
+              const V cur = bm.load(bw_env(bw), bw_slot(bw));
               rounds(std::integral_constant<int, 1>(), r0, &bw, &cur);
           }
         }
@@ -2486,14 +2533,14 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #endif
                 for (uint64_t todo = todo0; todo;)   // uniform
                     todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, hud, s_chain,
-                                                                  s_serial STAMP_PASS, pre);
+                                                                  s_serial, GlobalSink<T>{st} STAMP_PASS, pre);
                 wave_sync();
                 if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
                 if (active && s_serial[e]) {   // uniform over the quad; rare
                     const uint32_t kq = uint32_t(quad_bcast_i<1, LPE>(int(hkey)));   // (lane q == 1 has the key)
                     const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
                     const NextGame<S> ng = next_game<S>(p, hseed, kq, hk, hud, c, stream_ring_of(st, i));
-                    restart_env<T, S, PMAX, LPE>(p, st, i, ng, q);
+                    restart_env<T, S, PMAX, LPE>(p, st, i, ng, q, GlobalSink<T>{st});
                 }
             }
 #ifdef ASTRO_STAMPS
@@ -2588,7 +2635,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 
     // ---- index the wave's live bullets densely (bullets_begin); their first
     //      two rounds load during the physics below
-    const BulletsIn<T> bin = bullets_begin<T, LPE>(st, BC, lane, e, q, base, nb, np, t0, s_index, s_kept, s_hit, s_serial);
+    const BulletsGlobal<T> bgl{bullets, ships, planets, BC, NN, base};
+    const BulletsIn<T> bin = bullets_begin<T, LPE>(bgl, lane, e, q, nb, np, t0, s_index, s_kept, s_hit, s_serial);
     const int total = bin.total;
     STAMP(19);
     // key[397] of the next game's seed (first step of a game): a random
@@ -2768,7 +2816,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     STAMP(3);
     // ---- bullets (core.py:241-251, 264-266, 295-300): collide with the old
     //      bodies, move, cull, compact in place (bullets_rounds)
-    bullets_rounds<T, S, PMAX, LPE, (HELP || OPAQUE) ? 2 : 1>(p, st, bin, lane, e, q, base, nb, sxf, syf, mpxf, mpyf,
+    bullets_rounds<T, S, PMAX, LPE, (HELP || OPAQUE) ? 2 : 1>(p, bgl, bin, lane, e, q, nb, sxf, syf, mpxf, mpyf,
                                                               s_body, s_index, s_kept, s_hit, gp, gs STAMP_PASS);
     if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
         if (!wait_lds_word(s_box_all[wv].seen)) report_error(st, ASTRO_ERR_HEADER_WAIT, lane);
@@ -2898,7 +2946,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     if constexpr (!HELP)
     for (uint64_t todo = __ballot(need_reset); todo;)   // uniform
         todo = wave_reset_pass<T, S, PMAX, LPE>(p, st, todo, lane, is, pend_seed, pend_key, key_valid || p.key_table,
-                                           undrawn, s_chain, s_serial STAMP_PASS);
+                                           undrawn, s_chain, s_serial, GlobalSink<T>{st} STAMP_PASS);
     if (!HELP && auto_reset) {
         wave_sync();
         if (stats) c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));
@@ -2907,7 +2955,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[is];
             const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, undrawn, c,
                                                 stream_ring_of(st, is));
-            restart_env<T, S, PMAX, LPE>(p, st, is, ng, q);
+            restart_env<T, S, PMAX, LPE>(p, st, is, ng, q, GlobalSink<T>{st});
         }
     }
     STAMP(10);
@@ -3049,6 +3097,516 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
 }
 
 // ---------------------------------------------------------------------------
+// The resident rollout: astro_rollout's K ticks with the env state ON CHIP
+// (core.play's tick loop, core.py:377-410, for open-loop or on-device
+// controls).  A wave loads its envs once -- header, ships and planets into
+// the registers of the env's lanes (the quad/pair layout of quad_tick), the
+// live bullets into the wave's LDS rows -- steps them K ticks from there, and
+// stores them once at the end.  No state crosses memory between ticks, so a
+// tick is its arithmetic: no load round trip, no wait for the previous
+// tick's stores.  What a tick still sends to memory: its reward and done
+// (the launch's outputs), and, for the first steps of a game, the pending
+// seed's key gather and its seed-stream draw (check_pending, global stream
+// record and ring: rare, consumed at the end of the tick).  Finished games
+// are re-created in the same tick (wave_reset_pass into an LDS stage the
+// env's lanes then read; the serial create into the lanes' own registers).
+// Float32 state with b_cap <= RES_BCAP only (the LDS rows); other rollouts
+// run quad_tick's K-tick instance.  Results are those of K astro_step
+// launches, bit for bit, on every state array (tests/test_gpu_parity.py
+// test_rollout_equals_stepping): every slot the launch writes in LDS is
+// stored back, and a slot it never wrote is left as it was.
+
+constexpr int RES_QWIN = 256;   // live bullets per LDS index window (a wave holds up to 32 x 32)
+constexpr int RES_WPG = 4;      // waves per workgroup; two workgroups per CU fit the LDS
+
+// One lane's part of its env across the launch (quad/pair layout): the header
+// (every lane of the env), its own ship (lanes q < S), its planet slots
+// q + LPE m, and how far into the env's bullet row the launch has written.
+template <typename T, int S, int PMAX, int LPE>
+struct ResEnv {
+    using V = typename Store<T>::V;
+    int4 h;
+    V sv;
+    T sb;
+    V pv[PMAX / LPE];
+    int hw;   // slots [0, hw) of the env's LDS row were written by this launch (or loaded)
+};
+
+// A reset pass's new game, one per row of the pass (LDS, over the wave's
+// body rows, which are free once the bullet pass is over).
+template <int S, int PMAX>
+struct ResStage {
+    float4 ship[S];
+    float b[4];
+    float4 planet[PMAX];
+    int4 hdr;
+};
+
+// Reset-pass sink: row r of the pass writes its env's new game into stage[r]
+template <typename T, int S, int PMAX>
+struct StageSink {
+    using V = typename Store<T>::V;
+    ResStage<S, PMAX> *stage;
+    __device__ void ship(int s, int, const V &v, T b) const {
+        stage->ship[s] = make_float4(v.x, v.y, v.z, v.w);
+        stage->b[s] = b;
+    }
+    __device__ void planet(int j, int, int, const V &v) const { stage->planet[j] = make_float4(v.x, v.y, v.z, v.w); }
+    __device__ void header(int, const int4 &h) const { stage->hdr = h; }
+    __device__ StageSink for_row(int r) const { return StageSink{stage + r}; }
+};
+
+// Serial-create sink (create_env with NPART = LPE, part = q): the lane's own
+// ship and planet slots go straight into its registers
+template <typename T, int S, int PMAX, int LPE>
+struct RegSink {
+    using V = typename Store<T>::V;
+    ResEnv<T, S, PMAX, LPE> *r;
+    __device__ void ship(int, int, const V &v, T b) const {
+        r->sv = v;
+        r->sb = b;
+    }
+    __device__ void planet(int, int m, int, const V &v) const { r->pv[m] = v; }
+    __device__ void header(int, const int4 &h) const { r->h = h; }
+};
+
+template <int LPE>
+__device__ __forceinline__ int4 group_bcast0(const int4 &v) {   // lane 0 of the env's group to the group
+    return make_int4(quad_bcast_i<0, LPE>(v.x), quad_bcast_i<0, LPE>(v.y), quad_bcast_i<0, LPE>(v.z),
+                     quad_bcast_i<0, LPE>(v.w));
+}
+
+// One tick of a resident wave (quad_tick's physics, the state from R and the
+// wave's LDS rows).  ctl: this lane's control for the tick.
+template <typename T, int S, int PMAX, int LPE>
+__device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState &st, float *__restrict__ reward_all,
+                                         uint8_t *__restrict__ done_all, int auto_reset, int kt, int ctl, int lane,
+                                         int base, ResEnv<T, S, PMAX, LPE> &R, lds_f4 *rows,
+                                         float4 (*s_body)[(S + PMAX + 1) / 2], uint32_t *s_index, int *s_kept,
+                                         int *s_hit, int *s_serial, QuadCounts &cnt) {
+    using V = typename Store<T>::V;
+    static_assert(std::is_same<T, float>::value, "the resident rollout holds float32 state");
+    constexpr int PPL = PMAX / LPE;
+    constexpr int NBOD2 = (S + PMAX + 1) / 2;
+    const int q = lane & (LPE - 1);
+    const int e = lane / LPE;
+    const int N = st.n_env;
+    const size_t NN = size_t(N);
+    const bool active = base + e < N;
+    const int i = active ? base + e : N - 1;
+    float *__restrict__ reward = reward_all + size_t(kt) * NN * S;
+    uint8_t *__restrict__ done_out = done_all + size_t(kt) * NN;
+    bool f_reset = false, f_coll = false, f_tout = false, need_reset = false;
+
+    // ---- the state, from registers
+    const int4 h = R.h;
+    const V sv = R.sv;
+    const T sbv = R.sb;
+    V pv[PPL];
+    T mpx[PPL], mpy[PPL];
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) {
+        pv[m] = R.pv[m];
+        mpx[m] = pv[m].x;
+        mpy[m] = pv[m].y;
+    }
+    const int tick = int(uint32_t(h.x) & TICK_MASK);
+    const bool key_valid = (uint32_t(h.z) & KEY_VALID) != 0;
+    const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
+    uint32_t pend_seed = uint32_t(h.z) & SEED_MASK;
+    int np = h.y & 0xff;
+    const int flags = (h.y >> 8) & 0xff;
+    const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
+    np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
+    const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
+    const bool live = tick < p.timeout_tick;
+    const bool t0 = tick == 0;
+    const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
+    uint32_t pend_key = uint32_t(h.w);
+    cnt.n_pl += active && q == 0 ? uint32_t(np) : 0u;
+    float rw_out = 0.0f;   // this tick's reward (lanes q < S) and done (q == 0), stored last
+    uint8_t done_v = 0;
+
+    // ---- the wave's live bullets numbered densely, first rounds read (LDS)
+    const BulletsLds<S, NBOD2> bm{rows, lds_ptr(&s_body[0][0])};
+    const BulletsIn<T> bin = bullets_begin<T, LPE, RES_QWIN>(bm, lane, e, q, nb, np, t0, s_index, s_kept, s_hit,
+                                                             s_serial);
+    // the pending seed's key gather and stream cursor (check_pending, a
+    // game's first steps): issued now, consumed at the end of the tick
+    if (q == 0 && !key_valid && !undrawn && p.key_table) pend_key = p.key_table[pend_seed & SEED_MASK];
+    const bool want_c = q == 0 && (undrawn || (!key_valid && p.key_table && p.planets_only));
+    uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
+    asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // (as quad_tick: loaded branch-free)
+    const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
+
+    // ---- broadcasts, own ship's direction, thrust + gravity (core.py:234-239)
+    double px[PMAX], py[PMAX], sx[S], sy[S];
+    bcast_slots<T, PPL, LPE>(mpx, px);
+    bcast_slots<T, PPL, LPE>(mpy, py);
+    sx[0] = double(quad_bcast<0, LPE>(sv.x));
+    sy[0] = double(quad_bcast<0, LPE>(sv.y));
+    if (S == 2) {
+        sx[S - 1] = double(quad_bcast<S - 1, LPE>(sv.x));
+        sy[S - 1] = double(quad_bcast<S - 1, LPE>(sv.y));
+    }
+    const double mx = double(sv.x), my = double(sv.y), mdx = double(sv.z), mdy = double(sv.w);
+    const double mb = double(sbv);
+    float ds, dc;
+    np_sincosf(float(mb), ds, dc);
+    double ax = 0.0, ay = 0.0;
+    double sgx = 0.0, sgy = 0.0;
+    if constexpr (LPE == 4 && PMAX == 4) {   // the ships' fields split over the quad (as quad_tick)
+        double s0x = sx[0], s0y = sy[0], s1x = sx[S - 1], s1y = sy[S - 1];
+        double p0x = px[0], p0y = py[0], p1x = px[1], p1y = py[1], p2x = px[2], p2y = py[2], p3x = px[3], p3y = py[3];
+        asm volatile("" : "+v"(s0x), "+v"(s0y), "+v"(s1x), "+v"(s1y));
+        asm volatile("" : "+v"(p0x), "+v"(p0y), "+v"(p1x), "+v"(p1y), "+v"(p2x), "+v"(p2y), "+v"(p3x), "+v"(p3y));
+        const bool odd = (q & 1) != 0, hi = q >= 2;
+        const double shx = odd ? s1x : s0x, shy = odd ? s1y : s0y;
+        const double ax_ = hi ? p1x : p0x, ay_ = hi ? p1y : p0y;
+        const double bx_ = hi ? p3x : p2x, by_ = hi ? p3y : p2y;
+        const double rax = ax_ - shx, ray = ay_ - shy, rbx = bx_ - shx, rby = by_ - shy;
+        const double fa = div_gravity(p.gm, max_floor(rax * rax + ray * ray));
+        const double fb = div_gravity(p.gm, max_floor(rbx * rbx + rby * rby));
+        const double tax = fa * rax, tay = fa * ray, tbx = fb * rbx, tby = fb * rby;
+        const double t1x = quad_perm_d<2, 3, 2, 3>(tax), t1y = quad_perm_d<2, 3, 2, 3>(tay);
+        const double t3x = quad_perm_d<2, 3, 2, 3>(tbx), t3y = quad_perm_d<2, 3, 2, 3>(tby);
+        sgx = tax;
+        sgy = tay;
+        sgx = 1 < np ? sgx + t1x : sgx;
+        sgy = 1 < np ? sgy + t1y : sgy;
+        sgx = 2 < np ? sgx + tbx : sgx;
+        sgy = 2 < np ? sgy + tby : sgy;
+        sgx = slot_last && 3 < np ? sgx + t3x : sgx;
+        sgy = slot_last && 3 < np ? sgy + t3y : sgy;
+    }
+    if (q < S) {
+        double gx, gy;
+        if (t0) {
+            float fx, fy;
+            field<float, PMAX>(px, py, np, mx, my, p.gm, fx, fy);
+            gx = double(fx);
+            gy = double(fy);
+        } else if constexpr (LPE == 4 && PMAX == 4) {
+            gx = sgx;
+            gy = sgy;
+        } else {
+            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
+        }
+        const double thr = p.thrust * double(ctl & 1);
+        ax = thr * double(ds) + gx;
+        ay = thr * double(dc) + gy;
+    }
+
+    // ---- ship collisions (core.py:241-253)
+    const Guard gsp(p.r2_sp), gss(p.r2_ss), gp(p.r2_p0), gs(p.r2_s0);
+    float sxf[S], syf[S], mpxf[PPL], mpyf[PPL];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        sxf[s] = float(sx[s]);
+        syf[s] = float(sy[s]);
+    }
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) {
+        mpxf[m] = q + LPE * m < np ? float(mpx[m]) : -FAR_POS;
+        mpyf[m] = q + LPE * m < np ? float(mpy[m]) : -FAR_POS;
+    }
+    bool hsp[S];
+    {
+        bool amb = false;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            bool hs = false;
+#pragma unroll
+            for (int m = 0; m < PPL; ++m) hs |= near32_t0(sxf[s], syf[s], mpxf[m], mpyf[m], gsp, amb, t0);
+            hsp[s] = hs;
+        }
+        bool hh = false;
+        if (S == 2 && q == 0) hh = near32_t0(sxf[0], syf[0], sxf[S - 1], syf[S - 1], gss, amb, t0);
+        if (__any(amb)) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                bool hs = false;
+#pragma unroll
+                for (int m = 0; m < PPL; ++m)
+                    hs |= (q + LPE * m < np) & closer_exact(sx[s], sy[s], double(mpx[m]), double(mpy[m]), gsp, t0);
+                hsp[s] = amb ? hs : hsp[s];
+            }
+            if (S == 2 && q == 0) hh = amb ? closer_exact(sx[0], sy[0], sx[S - 1], sy[S - 1], gss, t0) : hh;
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) hsp[s] = hsp[s] || hh;
+    }
+
+    // ---- bullets (core.py:241-251, 264-266, 295-300), in the LDS rows
+    bullets_rounds<T, S, PMAX, LPE, 2, RES_QWIN>(p, bm, bin, lane, e, q, nb, sxf, syf, mpxf, mpyf, s_body, s_index,
+                                                 s_kept, s_hit, gp, gs);
+    const int wr_in = s_kept[e];
+    const int hit_bits = s_hit[e];
+    cnt.n_bin += active && q == 0 ? uint32_t(nb) : 0u;
+    R.hw = max(R.hw, wr_in);   // (the pass compacted the row's first wr_in slots, finished game or not)
+
+    if (active) {
+        bool hit[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) hit[s] = quad_any<LPE>(hsp[s], lane) || ((hit_bits >> s) & 1);
+        const bool collided = S == 2 ? (hit[0] || hit[S - 1]) : hit[0];
+        const bool timeout = !collided && !live;
+        const uint8_t done = collided ? 1 : (timeout ? 2 : 0);
+        // rewards (core.py:253-260); stored at the end of the tick, after
+        // the tick's last wait for its own loads (a store issued before a
+        // wait for every memory op in flight would be waited for there)
+        const bool mh = q == 0 ? hit[0] : hit[S - 1];
+        rw_out = collided ? (mh ? -1.0f : 1.0f) : (timeout ? p.timeout_reward : 0.0f);
+        done_v = done;
+
+        if (!done) {   // uniform over the env's lanes
+            // ---- fire: ship s's bullet after the survivors, in ship order (core.py:267-280)
+            int wr = wr_in;
+            if ((fire_word >> (tick & 31)) & 1u) {
+                bool keep = false;
+                V out;
+                if (q < S) {
+                    const float os = p.spawn_off * ds, oc = p.spawn_off * dc;
+                    const float vs = p.bullet_speed * ds, vc = p.bullet_speed * dc;
+                    if (t0) {
+                        const float dtf = float(p.dt);
+                        const float bx = float(mx) + os, by = float(my) + oc;
+                        const float bdx = (float(mdx) + vs) + 0.0f, bdy = (float(mdy) + vc) + 0.0f;
+                        const float nx = bx + dtf * bdx, ny = by + dtf * bdy;
+                        keep = (-1.0f <= nx && nx <= 1.0f) || (-1.0f <= ny && ny <= 1.0f);
+                        out.x = T(nx);
+                        out.y = T(ny);
+                        out.z = T(bdx);
+                        out.w = T(bdy);
+                    } else {
+                        const double bx = mx + double(os), by = my + double(oc);
+                        const double bdx = (mdx + double(vs)) + 0.0, bdy = (mdy + double(vc)) + 0.0;
+                        const double nx = bx + p.dt * bdx, ny = by + p.dt * bdy;
+                        keep = (-1.0 <= nx && nx <= 1.0) || (-1.0 <= ny && ny <= 1.0);
+                        out.x = T(nx);
+                        out.y = T(ny);
+                        out.z = T(bdx);
+                        out.w = T(bdy);
+                    }
+                }
+                const uint64_t nib = (__ballot(keep) >> (lane & ~(LPE - 1))) & ((1ull << LPE) - 1);
+                const int pos = wr + __popcll(nib & ((1ull << q) - 1));
+                if (keep && pos < p.b_cap) bm.store(e, pos, out);
+                wr += __popcll(nib);
+            }
+            const int w = wr < p.b_cap ? wr : p.b_cap;
+            const int dropped = wr - w;
+            R.hw = max(R.hw, w);
+
+            // ---- own ship: semi-implicit Euler + wrap (core.py:283-288)
+            if (q < S) {
+                const double ndx = mdx + ax * p.dt;
+                const double ndy = mdy + ay * p.dt;
+                V v;
+                v.x = T(wrap_unit<double>(mx + p.dt * ndx));
+                v.y = T(wrap_unit<double>(my + p.dt * ndy));
+                v.z = T(ndx);
+                v.w = T(ndy);
+                R.sv = v;
+                R.sb = T(mb + p.db * double((ctl >> 1) - 1));
+            }
+            // ---- own planets (core.py:289-294)
+            {
+                V pout[PPL];
+                planet_update<T, S, PMAX, LPE, PPL>(p, pv, mpx, mpy, q, np, t0, slot_last, pout);
+#pragma unroll
+                for (int m = 0; m < PPL; ++m)
+                    if (q + LPE * m < np) R.pv[m] = pout[m];
+            }
+            // ---- header: the pending seed checked by lane 0 (check_pending), to every lane
+            const int fl = flags | (dropped ? 1 : 0);
+            uint32_t kv = 0;
+            if (q == 0) kv = check_pending(p, st, i, key_valid, undrawn, c_pend, pend_seed, pend_key);
+            const int w2 = quad_bcast_i<0, LPE>(int(pend_seed | kv)), w3 = quad_bcast_i<0, LPE>(int(pend_key));
+            R.h = make_int4(tick + 1, np | (fl << 8) | (w << 16), w2, w3);
+            if (q == 0) {
+                cnt.n_bout += uint32_t(w);
+                cnt.n_drop += uint32_t(dropped);
+            }
+        } else {
+            f_coll = q == 0 && collided;
+            f_tout = q == 0 && timeout;
+            need_reset = auto_reset && q == 0;
+            f_reset = need_reset;
+        }
+    }
+
+    // ---- auto-reset: reset passes (four games at a time) into the LDS stage,
+    //      each env's lanes then take their part of its new game
+    ResStage<S, PMAX> *stage = reinterpret_cast<ResStage<S, PMAX> *>(&s_body[0][0]);
+    static_assert(4 * sizeof(ResStage<S, PMAX>) <= sizeof(float4) * (64 / LPE) * NBOD2, "stage over the body rows");
+    uint32_t(*s_chain)[2][13 + 2 * S] = reinterpret_cast<uint32_t(*)[2][13 + 2 * S]>(s_index);
+    static_assert(4 * 2 * (13 + 2 * S) <= RES_QWIN, "the reset chains over the index window");
+    const StageSink<T, S, PMAX> ssink{stage};
+    for (uint64_t todo = __ballot(need_reset); todo;) {   // uniform
+        const uint64_t before = todo;
+        todo = wave_reset_pass<T, S, PMAX, LPE, false, StageSink<T, S, PMAX>>(
+            p, st, todo, lane, i, pend_seed, pend_key, key_valid || p.key_table, undrawn, s_chain, s_serial, ssink);
+        const uint64_t served = before & ~todo;
+        wave_sync();
+        const int ldr = lane & ~(LPE - 1);
+        if (((served >> ldr) & 1ull) && !s_serial[e]) {   // uniform over the env's lanes
+            const ResStage<S, PMAX> &g = stage[__popcll(served & ((1ull << ldr) - 1))];
+            const int4 nh = g.hdr;
+            const int sq = q < S ? q : 0;
+            const float4 shv = g.ship[sq];
+            R.sv = V{shv.x, shv.y, shv.z, shv.w};
+            R.sb = g.b[sq];
+            const int n_new = nh.y & 0xff;
+#pragma unroll
+            for (int m = 0; m < PPL; ++m) {
+                if (q + LPE * m < n_new) {
+                    const float4 pl = g.planet[q + LPE * m];
+                    R.pv[m] = V{pl.x, pl.y, pl.z, pl.w};
+                }
+            }
+            R.h = nh;
+        }
+        wave_sync();   // the stage is free for the next pass
+    }
+    if (auto_reset) {
+        wave_sync();
+        cnt.c_serial += __popcll(__ballot(active && q == 0 && s_serial[e]));
+        if (active && s_serial[e]) {   // uniform over the env's lanes; rare
+            const uint32_t kq = uint32_t(quad_bcast_i<0, LPE>(int(pend_key)));
+            const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
+            const NextGame<S> ng = next_game<S>(p, pend_seed, kq, key_valid || p.key_table, undrawn, c,
+                                                stream_ring_of(st, i));
+            restart_env<T, S, PMAX, LPE, RegSink<T, S, PMAX, LPE>>(p, st, i, ng, q, RegSink<T, S, PMAX, LPE>{&R});
+            R.h = group_bcast0<LPE>(R.h);   // (restart_env set the header on lane 0)
+        }
+    }
+    cnt.c_reset += __popcll(__ballot(f_reset));
+    cnt.c_coll += __popcll(__ballot(f_coll));
+    cnt.c_tout += __popcll(__ballot(f_tout));
+    if (active) {   // the tick's outputs
+        if (q < S) reward[size_t(i) * S + q] = rw_out;
+        if (q == 0) done_out[i] = done_v;
+    }
+}
+
+// Controls of the resident rollout: RANDOM / NOTHING / a control array
+// (the next tick's array entry loaded a tick ahead)
+template <typename T, int S, int PMAX, int LPE>
+__global__ __launch_bounds__(64 * RES_WPG, 2) void astro_rollout_res_kernel(AstroParams p, AstroState st,
+                                                                           TickDriver drv,
+                                                                           float *__restrict__ reward_all,
+                                                                           uint8_t *__restrict__ done_all,
+                                                                           unsigned long long *stats,
+                                                                           int auto_reset) {
+    using V = typename Store<T>::V;
+    constexpr int PPL = PMAX / LPE;
+    constexpr int QENV = 64 / LPE;
+    constexpr int NBOD2 = (S + PMAX + 1) / 2;
+    __shared__ float4 s_rows_all[RES_WPG][QENV * RES_BCAP];
+    __shared__ float4 s_body_all[RES_WPG][QENV][NBOD2];
+    __shared__ uint32_t s_index_all[RES_WPG][RES_QWIN];
+    __shared__ int s_kept_all[RES_WPG][QENV], s_hit_all[RES_WPG][QENV], s_serial_all[RES_WPG][QENV];
+    const int wv = int(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int q = lane & (LPE - 1);
+    const int e = lane / LPE;
+    const int N = st.n_env;
+    const size_t NN = size_t(N);
+    const int base = (blockIdx.x * RES_WPG + wv) * QENV;
+    if (base >= N) return;   // a spare wave of the last block (waves never wait for each other)
+    const bool active = base + e < N;
+    const int i = active ? base + e : N - 1;
+    const int sq = q < S ? q : 0;
+    lds_f4 *rows = lds_ptr(&s_rows_all[wv][0]);
+
+    // ---- load the wave's envs
+    ResEnv<T, S, PMAX, LPE> R;
+    R.h = reinterpret_cast<const int4 *>(st.hdr)[i];
+    R.sv = reinterpret_cast<const V *>(st.ships)[size_t(sq) * NN + i];
+    R.sb = reinterpret_cast<const T *>(st.ships_b)[size_t(sq) * NN + i];
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) {
+        const int j = q + LPE * m;
+        R.pv[m] = reinterpret_cast<const V *>(st.planets)[size_t(j < p.p_pad ? j : 0) * NN + i];
+    }
+    const int nb0 = active ? min(int(uint32_t(R.h.y) >> 16), p.b_cap) : 0;
+    R.hw = nb0;
+    {   // the env's live bullets into its LDS row, lane q taking slots q, q + LPE, ...
+        const V *brow = reinterpret_cast<const V *>(st.bullets) + size_t(i) * size_t(p.b_cap);
+        for (int k0 = 0; k0 < nb0; k0 += 4 * LPE) {
+            V v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + q + LPE * u;
+                v[u] = brow[k < nb0 ? k : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + q + LPE * u;
+                if (k < nb0) {
+                    v4f w;
+                    w.x = v[u].x;
+                    w.y = v[u].y;
+                    w.z = v[u].z;
+                    w.w = v[u].w;
+                    rows[e * RES_BCAP + k] = w;
+                }
+            }
+        }
+    }
+    wave_sync();
+
+    // ---- the ticks (the arguments re-read from the kernarg segment each tick,
+    //      as the K-tick quad_tick instance does: scalar loads, not SGPRs
+    //      held across the loop)
+    QuadCounts cnt{};
+    const bool from_array = drv.policy == ASTRO_POLICY_CONTROL;
+    int ctl_next = from_array ? int(drv.control[size_t(i) * S + sq]) : 0;
+    const int n_ticks = drv.ticks;
+    for (int kt = 0; kt < n_ticks; ++kt) {
+        auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const QuadArgs &a = *(const QuadArgs *)(KernArgs(kp));
+        int ctl;
+        if (from_array) {   // uniform: this tick's entry (loaded a tick ago); the next one's issued
+            ctl = ctl_next;  // (the last tick re-reads its own: no branch around the load)
+            const int kn = kt + 1 < n_ticks ? kt + 1 : kt;
+            ctl_next = int(a.drv.control[(size_t(kn) * NN + size_t(i)) * S + sq]);
+        } else {
+            ctl = tick_control<S>(a.drv, i, sq, NN, kt);
+        }
+        res_tick<T, S, PMAX, LPE>(a.p, a.st, a.reward, a.done, a.auto_reset, kt, ctl, lane, base, R, rows,
+                                  s_body_all[wv], s_index_all[wv], s_kept_all[wv], s_hit_all[wv],
+                                  s_serial_all[wv], cnt);
+    }
+
+    // ---- store the wave's envs: every slot the launch wrote (padding
+    //      planet slots hold what was loaded: storing them changes nothing)
+    if (active) {
+        if (q == 0) reinterpret_cast<int4 *>(st.hdr)[i] = R.h;
+        if (q < S) {
+            reinterpret_cast<V *>(st.ships)[size_t(q) * NN + i] = R.sv;
+            reinterpret_cast<T *>(st.ships_b)[size_t(q) * NN + i] = R.sb;
+        }
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            const int j = q + LPE * m;
+            if (j < p.p_pad) reinterpret_cast<V *>(st.planets)[size_t(j) * NN + i] = R.pv[m];
+        }
+        V *brow = reinterpret_cast<V *>(st.bullets) + size_t(i) * size_t(p.b_cap);
+        for (int k = q; k < R.hw; k += LPE) {
+            const v4f w = rows[e * RES_BCAP + k];
+            brow[k] = V{w.x, w.y, w.z, w.w};
+        }
+    }
+    if (stats) {   // the launch's counters (sums over K ticks: unpacked)
+        const int row = __builtin_amdgcn_readfirstlane(int(blockIdx.x * RES_WPG + wv));
+        flush_counts(stats + size_t(row) * ASTRO_NSTATS, cnt, false);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Observation features: rl.ValueNetwork.get_features + to_batch
 // (rl.py:36-112), one lane per (env, row).  The bearing feature is
 // util.norm_angle(b) / pi (util.py:125-132) in the precision numpy uses: float32
@@ -3162,13 +3720,15 @@ __global__ __launch_bounds__(BLOCK) void astro_reset_kernel(AstroParams p, Astro
         const bool undrawn = (uint32_t(h.z) & UNDRAWN) != 0;
         const uint32_t key = (uint32_t(h.z) & KEY_VALID) ? uint32_t(h.w) : undrawn ? 0u : key397_of(p, seed);
         const uint4 c = reinterpret_cast<const uint4 *>(st.stream)[i];
-        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, undrawn, c, stream_ring_of(st, i)));
+        restart_env<T, S, PMAX>(p, st, i, next_game<S>(p, seed, key, true, undrawn, c, stream_ring_of(st, i)), 0,
+                                GlobalSink<T>{st});
         return;
     }
     // explicit seed: full chain now; the stream's pending game stays queued
     int cf = 0;
     const uint32_t seed = seeds[i];
-    const int n = create_env<T, S, PMAX>(p, st, i, create_draws<S>(create_words<S>(p, seed, key397_of(p, seed))), cf);
+    const int n = create_env<T, S, PMAX>(p, GlobalSink<T>{st}, i,
+                                         create_draws<S>(create_words<S>(p, seed, key397_of(p, seed))), cf);
     reinterpret_cast<int4 *>(st.hdr)[i] =
         make_int4(int(uint32_t(h.x) & ~TICK_MASK), n | ((cf ? 2 : 0) << 8), h.z, h.w);
     if (st.stream) reinterpret_cast<uint32_t *>(st.stream)[4 * i + 3] = seed;
@@ -3341,6 +3901,20 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
             }
             return launched(lpe == 4 ? "astro_step(quad, helpers)" : "astro_step(pair, helpers)");
         }
+#ifndef ASTRO_NO_RESIDENT   // (A/B builds only: every K-tick rollout on quad_tick's instance)
+        if constexpr (std::is_same<T, float>::value) {
+            if (!one && p.b_cap <= RES_BCAP) {   // K ticks with the state on chip
+                const int gr = int((int64_t(s.n_env) * lpe + 64 * RES_WPG - 1) / (64 * RES_WPG));
+                if (lpe == 4)
+                    hipLaunchKernelGGL((astro_rollout_res_kernel<T, S, PM, 4>), dim3(gr), dim3(64 * RES_WPG), 0,
+                                       stream, p, s, drv, r, d, st, ar);
+                else
+                    hipLaunchKernelGGL((astro_rollout_res_kernel<T, S, PM, 2>), dim3(gr), dim3(64 * RES_WPG), 0,
+                                       stream, p, s, drv, r, d, st, ar);
+                return launched(lpe == 4 ? "astro_rollout(quad, resident)" : "astro_rollout(pair, resident)");
+            }
+        }
+#endif
         if (lpe == 4 && one)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);

@@ -627,6 +627,49 @@ def test_rollout_equals_stepping(kernel, dtype):
     assert a.stat_dict() == b.stat_dict()
 
 
+RESIDENT_CASES = {
+    # (config, b_cap, p_pad, planets_only, auto_reset, ticks)
+    'overflow_no_reset': (CFG['rapid'], 6, 4, 0, False, 30),
+    'c3_filtered_long': (CFG['default'], 32, 4, 3, True, 150),
+    'eight_slots': (None, 16, 8, 0, True, 60),
+    'solo': (CFG['solo'], 8, 4, 0, True, 40),
+}
+
+
+@pytest.mark.parametrize('kernel', ['quad', 'pair'])
+@pytest.mark.parametrize('case', sorted(RESIDENT_CASES))
+def test_resident_rollout_equals_stepping(kernel, case):
+    """The resident rollout (float32 state, b_cap <= 32: the env state held
+    on chip for the launch's K ticks) == K astro_step launches bit for bit on
+    every state array -- dead bullet slots and padded planet slots included
+    -- and the same statistics: with bullets dropped for lack of b_cap and
+    no auto-reset (finished games re-stepped), on the 3-planet-filtered c3
+    workload long enough for every game's pending-seed checks and draws, and
+    with 8 planet slots (1-8 planets)."""
+    from astro_amd import BatchedEnv
+    cfg, b_cap, p_pad, only, ar, K = RESIDENT_CASES[case]
+    if cfg is None:
+        cfg = CFG['default']._replace(max_planets=8)
+    n = 1500
+    envs = [BatchedEnv(cfg, n, device='cuda:0', b_cap=b_cap, p_pad=p_pad, dtype=torch.float32,
+                       auto_reset=ar, kernel=kernel, planets_only=only, env_offset=77) for _ in range(2)]
+    for e in envs:
+        e.reset()
+        e.rollout(25, 'random', tick0=1 << 20, auto_reset=True)   # games of several ages first
+    a, b = envs
+    ctl = torch.from_numpy(np.random.RandomState(11).randint(0, 6, size=(K, n, a.S)).astype(np.int8)).cuda()
+    rew, done = a.rollout(K, ctl, auto_reset=ar)
+    for k in range(K):
+        _, r, d = b.step(ctl[k], auto_reset=ar)
+        assert torch.equal(rew[k], r) and torch.equal(done[k], d), k
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream', 'stream_ring'):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert a.stat_dict() == b.stat_dict()
+    assert int(done.ne(0).sum()) > 0
+    if case == 'overflow_no_reset':
+        assert int(((a.flags & 1) != 0).sum()) > 0   # bullets were dropped
+
+
 @pytest.mark.parametrize('kernel', KERNELS)
 def test_step_many_equals_stepping(kernel):
     """step_many(controls [K, N, S]) (astro_step_many: K one-tick launches
