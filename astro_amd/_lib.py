@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # (ASTRO_LIB: another build of the same library, e.g. an A/B variant from tools/build_var.sh)
 LIB_PATH = os.environ.get('ASTRO_LIB') or os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
@@ -83,6 +83,41 @@ class AstroPolicy(ctypes.Structure):
     ]
 
 
+class AstroGameTick(ctypes.Structure):
+    """include/astro_step.h AstroGameTick: one game's tick (astro_game_step)."""
+    _fields_ = [
+        ('params', AstroParams),
+        ('state', AstroState),
+        ('stream', ctypes.c_void_p),
+        ('hdr', ctypes.c_void_p),
+        ('ships', ctypes.c_void_p),
+        ('ships_b', ctypes.c_void_p),
+        ('planets', ctypes.c_void_p),
+        ('bullets', ctypes.c_void_p),
+        ('control', ctypes.c_void_p),
+        ('fire', ctypes.c_void_p),
+        ('reward', ctypes.c_void_p),
+        ('done', ctypes.c_void_p),
+        ('errors', ctypes.c_void_p),
+        ('control_dev', ctypes.c_void_p),
+        ('fire_dev', ctypes.c_void_p),
+        ('reward_dev', ctypes.c_void_p),
+        ('done_dev', ctypes.c_void_p),
+        ('in_', ctypes.c_void_p),
+        ('out', ctypes.c_void_p),
+        ('nplanets', ctypes.c_int32),
+        ('nbullets', ctypes.c_int32),
+        ('control0', ctypes.c_int32),
+        ('control1', ctypes.c_int32),
+        ('first_step', ctypes.c_int32),
+        ('fire_now', ctypes.c_int32),
+        ('timeout_now', ctypes.c_int32),
+        ('out_nbullets', ctypes.c_int32),
+        ('done_out', ctypes.c_int32),
+        ('reward_out', ctypes.c_float * 2),
+    ]
+
+
 POLICIES = {'control': 0, 'nothing': 1, 'random': 2, 'bots': 3}
 BOTS = {'nothing': 0, 'script': 1, 'random': 2}
 
@@ -110,6 +145,7 @@ _SYMBOLS = {
     'astro_host_free': (ctypes.c_int, [ctypes.c_void_p]),
     'astro_dev_alloc': (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     'astro_dev_free': (ctypes.c_int, [ctypes.c_void_p]),
+    'astro_game_step': (ctypes.c_int, [ctypes.c_void_p]),
     'astro_rollout': (ctypes.c_int, [ctypes.POINTER(AstroParams), ctypes.POINTER(AstroState),
                                      ctypes.POINTER(AstroPolicy), ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,

@@ -4225,6 +4225,95 @@ int astro_dev_free(void *device) {
     return e == hipSuccess ? 0 : fail(-1000 - int(e), "hipFree failed: %s", hipGetErrorString(e));
 }
 
+int astro_game_step(AstroGameTick *t) {
+    if (!t) return fail(-91, "tick record is NULL");
+    const int S = t->params.nships, np = t->nplanets, nb = t->nbullets;
+    if (S != 1 && S != 2) return fail(-11, "nships must be 1 or 2");
+    if (np < 1 || np > t->params.p_pad) return fail(-92, "nplanets must be in [1, p_pad]");
+    if (nb < 0 || nb > t->params.b_cap) return fail(-93, "nbullets must be in [0, b_cap]");
+    if (t->state.n_env != 1 || t->state.state_f64 != 1) return fail(-94, "the game arena is one float64 env");
+    const double *in = t->in;
+    // the input state into the arena, in the kernels' layout
+    for (int s = 0; s < S; ++s) {
+        double *v = t->ships + 4 * s;
+        v[0] = in[2 * s];
+        v[1] = in[2 * s + 1];
+        v[2] = in[2 * S + 2 * s];
+        v[3] = in[2 * S + 2 * s + 1];
+        t->ships_b[s] = in[4 * S + s];
+    }
+    const double *pin = in + 5 * S;
+    for (int j = 0; j < np; ++j) {
+        double *v = t->planets + 4 * j;
+        v[0] = pin[2 * j];
+        v[1] = pin[2 * j + 1];
+        v[2] = pin[2 * np + 2 * j];
+        v[3] = pin[2 * np + 2 * j + 1];
+    }
+    const double *bin = pin + 4 * np;
+    for (int k = 0; k < nb; ++k) {
+        double *v = t->bullets + 4 * k;
+        v[0] = bin[2 * k];
+        v[1] = bin[2 * k + 1];
+        v[2] = bin[2 * nb + 2 * k];
+        v[3] = bin[2 * nb + 2 * k + 1];
+    }
+    const int tick = t->first_step ? 0 : 1;
+    t->hdr[0] = int32_t((uint32_t(t->hdr[0]) & ~TICK_MASK) | uint32_t(tick));
+    t->hdr[1] = np | (nb << 16);
+    t->control[0] = int8_t(t->control0);
+    if (S == 2) t->control[1] = int8_t(t->control1);
+    t->fire[0] = uint32_t(t->fire_now ? 1 : 0) << tick;
+    AstroParams p = t->params;
+    p.timeout_tick = t->timeout_now ? tick : tick + 1;
+    p.fire_bits = t->fire_dev;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(t->stream);
+    int rc = astro_step(&p, &t->state, t->control_dev, t->reward_dev, t->done_dev, nullptr, 0, stream);
+    if (rc) return rc;
+    hipError_t e;
+    while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
+    }
+    if (e != hipSuccess) return fail(-1000 - int(e), "astro_game_step: %s", hipGetErrorString(e));
+    if (*t->errors) {
+        const uint32_t bits = *t->errors;
+        *t->errors = 0;
+        return fail(-90, "astro_step reported device error 0x%x", bits);
+    }
+    t->done_out = *t->done;
+    t->reward_out[0] = t->reward[0];
+    t->reward_out[1] = S == 2 ? t->reward[1] : 0.0f;
+    if (t->done_out) return 0;
+    // the next state, packed (the planets' count is the input's)
+    const int nb2 = int(uint32_t(t->hdr[1]) >> 16);
+    t->out_nbullets = nb2;
+    double *out = t->out;
+    for (int s = 0; s < S; ++s) {
+        const double *v = t->ships + 4 * s;
+        out[2 * s] = v[0];
+        out[2 * s + 1] = v[1];
+        out[2 * S + 2 * s] = v[2];
+        out[2 * S + 2 * s + 1] = v[3];
+        out[4 * S + s] = t->ships_b[s];
+    }
+    double *pout = out + 5 * S;
+    for (int j = 0; j < np; ++j) {
+        const double *v = t->planets + 4 * j;
+        pout[2 * j] = v[0];
+        pout[2 * j + 1] = v[1];
+        pout[2 * np + 2 * j] = v[2];
+        pout[2 * np + 2 * j + 1] = v[3];
+    }
+    double *bout = pout + 4 * np;
+    for (int k = 0; k < nb2; ++k) {
+        const double *v = t->bullets + 4 * k;
+        bout[2 * k] = v[0];
+        bout[2 * k + 1] = v[1];
+        bout[2 * nb2 + 2 * k] = v[2];
+        bout[2 * nb2 + 2 * k + 1] = v[3];
+    }
+    return 0;
+}
+
 int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_t rows, void *stream) {
     int rc = check_params(p);
     if (rc) return rc;

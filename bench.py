@@ -156,12 +156,20 @@ def single_game_latency(cfg, ticks=2000, seed=0):
     core.SHIM_MODE = default
     core._ENVS.clear()
     # the CPU comparison for this same path: oracle/port.py's core.step on
-    # one host core, the same config, random controls, re-create on termination
+    # one host core, the same config, the same loop (controls drawn up front,
+    # re-create on termination)
     from oracle import port
-    steps, secs = port.run_for(cfg, 2.0, seed=seed)
-    out['cpu_port_us_per_step'] = secs / steps * 1e6
+    g = port.Game(cfg)
+    ctl = np.random.RandomState(seed).randint(0, 6, size=(ticks, 2))
+    state = g.create(cfg.seed)
+    t0 = time.perf_counter()
+    for k in range(ticks):
+        state, _ = g.step(state, ctl[k])
+        if state is None:
+            state = g.create(cfg.seed)
+    out['cpu_port_us_per_step'] = (time.perf_counter() - t0) / ticks * 1e6
     out['cpu_port_sample'] = '%d core.step ticks of oracle/port.py on one host core, %s' % (
-        steps, 'DEFAULT_CONFIG' if cfg == DEFAULT_CONFIG else 'the same config')
+        ticks, 'DEFAULT_CONFIG' if cfg == DEFAULT_CONFIG else 'the same config')
     return out
 
 
@@ -173,9 +181,10 @@ def _single_game(core, cfg, ticks, seed):
         if state is None:
             state = core.create(cfg)
     n_create = 0
+    ctl = rng.randint(0, 6, size=(ticks, 2))   # (drawn up front, as the CPU comparison's loop)
     t0 = time.perf_counter()
-    for _ in range(ticks):
-        state, _ = core.step(state, rng.randint(0, 6, size=2), cfg)
+    for k in range(ticks):
+        state, _ = core.step(state, ctl[k], cfg)
         if state is None:
             state = core.create(cfg)
             n_create += 1
@@ -192,9 +201,10 @@ def _single_game(core, cfg, ticks, seed):
     return dict(us_per_step=dt / ticks * 1e6, steps=ticks, creates=n_create, us_per_play_tick=dp / played * 1e6,
                 play_ticks=played, games=k,
                 path='astro_amd.core.step (float64 state, bit-exact to the reference): "mapped" (default): the '
-                     'game in host memory the kernel addresses directly, one launch and one busy-polled event per '
-                     'tick; "copy": one H2D copy of the packed state, one launch, one D2H copy, one event; the CPU '
-                     'reference port (oracle/port.py) per tick on one core beside it')
+                     'game in host memory the kernel addresses directly, a tick one astro_game_step call (pack, '
+                     'launch, busy-wait, unpack in C); "copy": one H2D copy of the packed state, one launch, one D2H '
+                     'copy, one event; the CPU reference port (oracle/port.py) per tick on one core beside it, the '
+                     'same loop (controls drawn up front, re-create on termination)')
 
 
 def _free_port():

@@ -18,6 +18,8 @@
  *   astro_stream_init  <- core.generate_configs(config)       core.py:77-83
  *   astro_features     <- rl.ValueNetwork.get_features(state) + to_batch
  *                         (rl.py:36-112), the observation a policy consumes
+ *   astro_game_step    <- core.step for ONE game as server.py's game_tick calls it
+ *                         (server.py:41-51): state in, next state out, one call
  *
  * Conventions
  *   - The caller owns all memory the entry points read and write (e.g.
@@ -44,7 +46,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 19
+#define ASTRO_ABI_VERSION 20
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -252,6 +254,49 @@ int astro_features(const AstroParams *p, const AstroState *s, float *out, int32_
  * Every kernel access crosses PCIe: for one or a few games only. */
 int astro_host_alloc(uint64_t bytes, void **host, void **device);
 int astro_host_free(void *host);
+
+/* One tick of ONE game (core.step, core.py:215-303, as astro/server.py's
+ * game_tick and core.play call it), host state in and host state out in a
+ * single call: the packed input state is written into the game's arena (host
+ * memory the kernel addresses directly, astro_host_alloc), the step kernel
+ * runs on `stream`, the call spins until it has finished (hipStreamQuery)
+ * and packs the next state.  Packed state layout (float64, the reference
+ * State's arrays in order): ships x [S][2], dx [S][2], b [S]; planets x
+ * [nplanets][2], dx [nplanets][2]; bullets x [nbullets][2], dx [nbullets][2].
+ * Returns 0 (then done / reward / out / out_nbullets are set; out only when
+ * done == 0), a negative argument/launch code, or -90 when the launch set
+ * AstroState.errors bits (astro_last_error names them). */
+typedef struct AstroGameTick {
+    AstroParams params;     /* the game's config; the call sets timeout_tick and fire_bits */
+    AstroState state;       /* device addresses of the arena's arrays (n_env 1, state_f64 1) */
+    void *stream;
+    /* host addresses of the same arena bytes */
+    int32_t *hdr;
+    double *ships, *ships_b, *planets, *bullets;
+    int8_t *control;
+    uint32_t *fire;
+    float *reward;
+    uint8_t *done;
+    uint32_t *errors;
+    /* device addresses of control / fire / reward / done */
+    const int8_t *control_dev;
+    const uint32_t *fire_dev;
+    float *reward_dev;
+    uint8_t *done_dev;
+    const double *in;       /* host: the input state, packed */
+    double *out;            /* host: the next state, packed (room for b_cap bullets) */
+    /* this call */
+    int32_t nplanets, nbullets;
+    int32_t control0, control1;
+    int32_t first_step;     /* the game's first step (create()'s float32 arrays: tick 0) */
+    int32_t fire_now;       /* reload_time <= reload + dt          core.py:263-267 */
+    int32_t timeout_now;    /* max_time <= t + dt                  core.py:257 */
+    /* results */
+    int32_t out_nbullets;
+    int32_t done_out;       /* 0 running, 1 ship collision, 2 timeout */
+    float reward_out[2];
+} AstroGameTick;
+int astro_game_step(AstroGameTick *t);
 
 /* Device memory of a chosen kind, zeroed, for the per-step state arrays
  * (ships, ships_b, planets, bullets, hdr, reward, done).  A launch reads each

@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol(lib):
     assert set(names) == {'astro_abi_version', 'astro_last_error', 'astro_step', 'astro_step_many', 'astro_reset',
                           'astro_stream_init', 'astro_keytable_build', 'astro_features', 'astro_rollout',
                           'astro_controls', 'astro_host_alloc', 'astro_host_free', 'astro_dev_alloc',
-                          'astro_dev_free'}
+                          'astro_dev_free', 'astro_game_step'}
     out = subprocess.check_output(['nm', '-D', '--defined-only', _lib.LIB_PATH], text=True)
     exported = set(re.findall(r' T (astro_\w+)$', out, re.M))
     assert set(names) <= exported
@@ -48,11 +48,12 @@ def test_ctypes_struct_layout_matches_header():
     the ctypes mirrors'."""
     lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "astro_step.h"', 'int main(void){']
     expect = []
-    for st in (_lib.AstroParams, _lib.AstroState, _lib.AstroPolicy):
+    cname = {'in_': 'in'}   # (ctypes field names that are Python keywords)
+    for st in (_lib.AstroParams, _lib.AstroState, _lib.AstroPolicy, _lib.AstroGameTick):
         lines.append('printf("%%zu\\n", sizeof(%s));' % st.__name__)
         expect.append(ctypes.sizeof(st))
         for f, _ in st._fields_:
-            lines.append('printf("%%zu\\n", offsetof(%s, %s));' % (st.__name__, f))
+            lines.append('printf("%%zu\\n", offsetof(%s, %s));' % (st.__name__, cname.get(f, f)))
             expect.append(getattr(st, f).offset)
     lines.append('return 0;}')
     with tempfile.TemporaryDirectory() as d:
@@ -62,6 +63,22 @@ def test_ctypes_struct_layout_matches_header():
         subprocess.check_call(['gcc', '-std=c99', '-I', os.path.dirname(HEADER), src, '-o', exe])
         got = [int(x) for x in subprocess.check_output([exe], text=True).split()]
     assert got == expect
+
+
+def test_game_step_validation_without_gpu(lib):
+    """astro_game_step (the single-game tick) rejects a bad record before
+    touching the arena or the device."""
+    assert lib.astro_game_step(None) == -91
+    t = _lib.AstroGameTick()
+    t.params = _lib.AstroParams(nships=2, solo=0, p_pad=4, max_planets=4, b_cap=64)
+    t.state = _lib.AstroState(n_env=1, state_f64=1)
+    t.nplanets, t.nbullets = 5, 0
+    assert lib.astro_game_step(ctypes.byref(t)) == -92 and b'nplanets' in lib.astro_last_error()
+    t.nplanets, t.nbullets = 3, 65
+    assert lib.astro_game_step(ctypes.byref(t)) == -93
+    t.nbullets = 0
+    t.state.n_env = 2
+    assert lib.astro_game_step(ctypes.byref(t)) == -94
 
 
 def test_argument_validation_without_gpu(lib):
