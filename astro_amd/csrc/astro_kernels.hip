@@ -183,12 +183,30 @@ __device__ __forceinline__ C max_floor(C d2) {
 // field = gm / max(1e-12, |r|^2) * r  (a 1/r law in 2-D: no sqrt)
 template <typename C, int PMAX>
 __device__ __forceinline__ void field(const double (&px)[PMAX], const double (&py)[PMAX], int np,
-                                      double x, double y, double gm, C &gx, C &gy, bool last = true) {
+                                      double x, double y, double gm, C &gx, C &gy, bool last = true,
+                                      int np_uni = 0) {
     // every slot is evaluated (padded slots hold a copy of planet 0) and the
     // sum selects: a per-planet branch costs more than the arithmetic when
     // some lane of the wave has all PMAX planets anyway.  `last` (wave-
-    // uniform) false says no lane has PMAX planets: the last slot is skipped
+    // uniform) false says no lane has PMAX planets: the last slot is skipped.
+    // np_uni > 0 (wave-uniform): every lane has np_uni planets, no selects
     C ax = C(0), ay = C(0);
+    if (np_uni > 0) {
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+            if (j >= np_uni) break;
+            const C rx = C(px[j]) - C(x);
+            const C ry = C(py[j]) - C(y);
+            const C d2 = rx * rx + ry * ry;
+            const C f = div_gravity(C(gm), max_floor(d2));
+            const C tx = f * rx, ty = f * ry;
+            ax = j == 0 ? tx : ax + tx;
+            ay = j == 0 ? ty : ay + ty;
+        }
+        gx = ax;
+        gy = ay;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < PMAX; ++j) {
         if (j == PMAX - 1 && j > 0 && !last) break;
@@ -596,6 +614,7 @@ struct GlobalSink {
         reinterpret_cast<V *>(st.planets)[size_t(j) * size_t(st.n_env) + ie] = v;
     }
     __device__ void header(int ie, const int4 &h) const { reinterpret_cast<int4 *>(st.hdr)[ie] = h; }
+    __device__ void stream_seed(int ie, uint32_t seed) const { st.stream[4 * size_t(ie) + 3] = seed; }
     __device__ GlobalSink for_row(int) const { return *this; }   // (a reset pass's row r)
 };
 
@@ -787,8 +806,22 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
             stamp_[k == 0 ? 12 : 13] = t_;                                                \
         }                                                                                \
     } while (0)
-constexpr int NSTAMP = 24;   // 0-13 step sections, 14-15 placement, 16-19 reset pass, 20-22 helper wave
+constexpr int NSTAMP = 32;   // 0-13 step sections, 14-15 placement, 16-19 reset pass, 20-31 helper wave
+// helper-wave stamps: s_memrealtime (HSTAMP_R) and s_memtime (HSTAMP_T) into stamp_[k]
+#define HSTAMP_R(k) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[k])::"memory")
+#define HSTAMP_T(k)                                                                                   \
+    do {                                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[k])::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+    } while (0)
 #else
+#define HSTAMP_R(k) \
+    do {            \
+    } while (0)
+#define HSTAMP_T(k) \
+    do {            \
+    } while (0)
 #define STAMP(k) \
     do {         \
     } while (0)
@@ -1528,6 +1561,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 constexpr int QWIN = 1024;        // live bullets per window of the quad kernel's LDS index
 
+
 // Inclusive prefix sum over the 64 lanes of a wave (all lanes active): DPP
 // row shifts inside each row of 16, then the row totals.
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
@@ -1760,7 +1794,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
     STAMP(18);
     if (on && fast) {
         if (u == 0) {   // the stream record's game seed and the header, as restart_env
-            st.stream[4 * size_t(ie) + 3] = seed;
+            sink.stream_seed(ie, seed);
             sink.header(ie, make_int4(0, n | (cf ? 2 << 8 : 0), int(UNDRAWN), 0));
         }
     }
@@ -1777,6 +1811,14 @@ struct QuadCounts {
 };
 
 
+// The value every lane of the wave holds, or 0 when they differ (wave-uniform,
+// in an SGPR: a uniform planet count lets the sums drop their per-lane
+// k < np selects, e.g. config 3's 3-planet games)
+__device__ __forceinline__ int wave_uniform_count(int v) {
+    const int v0 = __builtin_amdgcn_readfirstlane(v);
+    return __builtin_amdgcn_readfirstlane(int(__all(v == v0))) ? v0 : 0;
+}
+
 // One tick of the quad kernel's wave (16 envs), tick kt of the launch.
 // The surviving envs' planet update (core.py:289-294): gravity of all
 // planets incl. self, in the reference's order; float32 at tick 0 / for a
@@ -1789,6 +1831,7 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
                                               const T (&mpx)[PPL], const T (&mpy)[PPL], int q, int np, bool t0,
                                               bool slot_last, typename Store<T>::V (&out)[PPL]) {
     using V = typename Store<T>::V;
+    const int np_uni = wave_uniform_count(np);
     const float dtf = float(p.dt);
     double px[PMAX], py[PMAX];
     {   // the planets again from the quad (DPP) rather than 2*PMAX
@@ -1827,7 +1870,7 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
         const double B = slot_last ? fac(0, 3, 2, 3) : 0.0;
         const double C = fac(0, 2, 1, 3);
         const double A2 = pair_swap(A), B2 = pair_swap(B);   // lane 0: F12, F23; lane 1: F01, F03
-        const double z = 0.0;   // (self: unused)
+        const double z = p.gm;   // (self: any finite factor of gm's sign, see below)
         // planet q:     lane 0 [-, F01, F02, F03]   lane 1 [F10, -, F12, F13]
         // planet q + 2: lane 0 [F20, F21, -, F23]   lane 1 [F30, F31, F32, -]
         Fr[0][0] = l0 ? z : A2;
@@ -1853,8 +1896,8 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
         const double C = quad_perm_d<3, 0, 1, 2>(A);                              // F(q, q + 3)
 #pragma unroll
         for (int k = 0; k < PMAX; ++k) {
-            const int d = (k - q) & 3;   // (self, d == 0: unused)
-            Fr[0][k] = d == 1 ? A : (d == 2 ? B : C);
+            const int d = (k - q) & 3;   // (self, d == 0: gm, see below)
+            Fr[0][k] = d == 1 ? A : (d == 2 ? B : (d == 3 ? C : p.gm));
         }
     }
     // Pair kernel, 8 slots (config 5): the 28 distinct pair factors, 14 per
@@ -1883,7 +1926,7 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
         double Sf[PPL][PPL], Xf[PPL][PPL];
 #pragma unroll
         for (int a = 0; a < PPL; ++a) {
-            Sf[a][a] = 0.0;   // (self: unused)
+            Sf[a][a] = p.gm;   // (self: gm, see below)
 #pragma unroll
             for (int b = a + 1; b < PPL; ++b) {
                 Sf[a][b] = Sf[b][a] = fac(ox[a], oy[a], ox[b], oy[b]);
@@ -1937,21 +1980,31 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
 #else
                     if constexpr ((LPE == 2 && (PMAX == 4 || PMAX == 8)) || (LPE == 4 && PMAX == 4)) {
                         // field<double> at planet j from the shared factors:
-                        // term k = F(j, k) * (p_k - p_j) summed in k order; the
-                        // self term is gm / 1e-12 * (+0), a zero with gm's sign
-                        const double zs = __builtin_signbit(p.gm) ? -0.0 : 0.0;
+                        // term k = F(j, k) * (p_k - p_j) summed in k order.  The
+                        // self term is the reference's gm / 1e-12 * (+0): a zero
+                        // with gm's sign, which the table's self factor (gm
+                        // itself) times p_j - p_j = +0 gives exactly
                         double ax = 0.0, ay = 0.0;
+                        if (PMAX <= 4 && np_uni == PMAX - 1) {   // uniform: every env of the wave has PMAX - 1 planets
 #pragma unroll
-                        for (int k = 0; k < PMAX; ++k) {
-                            const bool self = k == j;
-                            const double tx = self ? zs : Fr[m][k] * (px[k] - pxj);
-                            const double ty = self ? zs : Fr[m][k] * (py[k] - pyj);
-                            if (k == 0) {
-                                ax = tx;
-                                ay = ty;
-                            } else {
-                                ax = k < np ? ax + tx : ax;
-                                ay = k < np ? ay + ty : ay;
+                            for (int k = 0; k < PMAX - 1; ++k) {
+                                const double tx = Fr[m][k] * (px[k] - pxj);
+                                const double ty = Fr[m][k] * (py[k] - pyj);
+                                ax = k == 0 ? tx : ax + tx;
+                                ay = k == 0 ? ty : ay + ty;
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < PMAX; ++k) {
+                                const double tx = Fr[m][k] * (px[k] - pxj);
+                                const double ty = Fr[m][k] * (py[k] - pyj);
+                                if (k == 0) {
+                                    ax = tx;
+                                    ay = ty;
+                                } else {
+                                    ax = k < np ? ax + tx : ax;
+                                    ay = k < np ? ay + ty : ay;
+                                }
                             }
                         }
                         gx = ax;
@@ -2024,6 +2077,63 @@ __device__ __forceinline__ bool wait_lds_word(const uint32_t &w) {
 __device__ __forceinline__ void report_error(const AstroState &st, uint32_t bits, int lane) {
     if (st.errors && lane == 0) atomicOr(st.errors, bits);
 }
+
+// One lane's part of its env across the launch (quad/pair layout): the header
+// (every lane of the env), its own ship (lanes q < S), its planet slots
+// q + LPE m, and how far into the env's bullet row the launch has written.
+template <typename T, int S, int PMAX, int LPE>
+struct ResEnv {
+    using V = typename Store<T>::V;
+    int4 h;
+    V sv;
+    T sb;
+    V pv[PMAX / LPE];
+    int hw;   // slots [0, hw) of the env's LDS row were written by this launch (or loaded)
+};
+
+// A new game made by a reset pass into LDS instead of the state arrays: the
+// resident rollout's (one per row of the pass, over the wave's body rows,
+// which are free once the bullet pass is over), and a helper wave's early
+// creates (games that end by a ship collision or the timeout, made before the
+// step wave posts and stored after it).  Float32 state.
+template <int S, int PMAX>
+struct ResStage {
+    float4 ship[S];
+    float b[4];
+    float4 planet[PMAX];
+    int4 hdr;
+    uint32_t seed;   // the stream record's current-game seed (stream[4 i + 3])
+    uint32_t pad[3];
+};
+
+// Reset-pass sink: row r of the pass writes its env's new game into stage[r]
+template <typename T, int S, int PMAX>
+struct StageSink {
+    using V = typename Store<T>::V;
+    ResStage<S, PMAX> *stage;
+    __device__ void ship(int s, int, const V &v, T b) const {
+        stage->ship[s] = make_float4(v.x, v.y, v.z, v.w);
+        stage->b[s] = b;
+    }
+    __device__ void planet(int j, int, int, const V &v) const { stage->planet[j] = make_float4(v.x, v.y, v.z, v.w); }
+    __device__ void header(int, const int4 &h) const { stage->hdr = h; }
+    __device__ void stream_seed(int, uint32_t seed) const { stage->seed = seed; }
+    __device__ StageSink for_row(int r) const { return StageSink{stage + r}; }
+};
+
+// Serial-create sink (create_env with NPART = LPE, part = q): the lane's own
+// ship and planet slots go straight into its registers
+template <typename T, int S, int PMAX, int LPE>
+struct RegSink {
+    using V = typename Store<T>::V;
+    ResEnv<T, S, PMAX, LPE> *r;
+    __device__ void ship(int, int, const V &v, T b) const {
+        r->sv = v;
+        r->sb = b;
+    }
+    __device__ void planet(int, int m, int, const V &v) const { r->pv[m] = v; }
+    __device__ void header(int, const int4 &h) const { r->h = h; }
+};
 
 // ---------------------------------------------------------------------------
 // The dense bullet pass of the quad/pair kernels (core.py:241-251, 264-266,
@@ -2103,7 +2213,11 @@ struct BulletsLds {
     }
 };
 
-template <typename T, int LPE, int QWN = QWIN, class BM>
+// EAGER (default): the first two rounds' bullets are loaded here, to fly
+// during the physics; otherwise (the helper-less one-tick instance of
+// millions of envs, where occupancy hides the latency and the registers held
+// across the physics cost a wave per SIMD) bullets_rounds loads them.
+template <typename T, int LPE, int QWN = QWIN, bool EAGER = true, class BM>
 __device__ __forceinline__ BulletsIn<T> bullets_begin(const BM &bm, int lane, int e, int q, int nb, int np, bool t0,
                                                       uint32_t *s_index, int *s_kept, int *s_hit, int *s_serial) {
     using V = typename Store<T>::V;
@@ -2127,18 +2241,20 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const BM &bm, int lane, in
         return b;
     }
     index_window<LPE, QWN>(s_index, 0, b.off, nb, q, b.tag);
-    wave_sync();
-    b.bw0 = lane < b.total ? s_index[lane] : 0u;
-    b.bw1 = lane + 64 < min(b.total, QWN) ? s_index[lane + 64] : 0u;
-    b.cur0 = bm.load(bw_env(b.bw0), bw_slot(b.bw0));
-    b.cur1 = bm.load(bw_env(b.bw1), bw_slot(b.bw1));
+    if constexpr (EAGER) {
+        wave_sync();
+        b.bw0 = lane < b.total ? s_index[lane] : 0u;
+        b.bw1 = lane + 64 < min(b.total, QWN) ? s_index[lane + 64] : 0u;
+        b.cur0 = bm.load(bw_env(b.bw0), bw_slot(b.bw0));
+        b.cur1 = bm.load(bw_env(b.bw1), bw_slot(b.bw1));
+    }
     return b;
 }
 
 // sxf/syf: both ships' old positions (float32); mpxf/mpyf: the lane's own
 // planet slots q + LPE m (float32, slots past the env's planets parked at
 // -FAR_POS).  Ends with the wave's LDS results readable (wave_sync).
-template <typename T, int S, int PMAX, int LPE, int NRW = 2, int QWN = QWIN, class BM>
+template <typename T, int S, int PMAX, int LPE, int NRW = 2, int QWN = QWIN, bool EAGER = true, class BM>
 __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const BM &bm, const BulletsIn<T> &b,
                                                int lane, int e, int q, int nb, const float (&sxf)[S],
                                                const float (&syf)[S], const float (&mpxf)[PMAX / LPE],
@@ -2155,6 +2271,13 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const BM &b
     if (total == 0) {   // uniform: nothing to do (bullets_begin left s_kept, s_hit cleared)
         wave_sync();
         return;
+    }
+    if constexpr (!EAGER) {   // the first two rounds' index words and bullets, now
+        wave_sync();
+        bw0 = lane < total ? s_index[lane] : 0u;
+        bw1 = lane + 64 < min(total, QWN) ? s_index[lane + 64] : 0u;
+        cur0 = bm.load(bw_env(bw0), bw_slot(bw0));
+        cur1 = bm.load(bw_env(bw1), bw_slot(bw1));
     }
     // ---- old positions of the env's bodies for the bullet pass (LDS)
     {
@@ -2375,6 +2498,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     __shared__ uint32_t s_chain_all[WPG][4][2][13 + 2 * S];   // init-key chains of a reset pass, see below
     __shared__ HelpBox s_box_all[HELP ? WPG : 1];
     __shared__ uint32_t s_pre_all[HELP ? WPG : 1][HELP ? QENV : 1][2][13 + 2 * S];   // a helper's chains, made ahead
+
     // (wave_sync syncs one wave whenever the build's QW > 1, whatever this instance's WPG)
     static_assert(!HELP || (QW > 1 && !OPAQUE), "helper waves: one-tick launches, wave-scoped LDS sync");
     // The helper waves check their step waves' pending seeds (check_pending's
@@ -2416,6 +2540,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         __syncthreads();
         if (base >= N) return QuadCounts{};
         if (helper) {
+            HSTAMP_R(23);
+            HSTAMP_T(24);
             // While its step wave steps, the helper makes the MT19937 init-key
             // chains of every env's pending game (the first 13 + 2S words from
             // the seed and from key[397]; 2 lanes per env, all envs at once):
@@ -2431,6 +2557,10 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             // launch's input whatever the memory system's timing (the store
             // depends on the loaded value: it waits for the load's return)
             if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
+#ifdef ASTRO_PROBE_IDLE_HELPERS   // measurement build only (wrong results): helpers only handshake
+            if (!wait_lds_word(bx.flag)) report_error(st, ASTRO_ERR_HELPER_WAIT, lane);
+            return QuadCounts{};
+#endif
             const uint32_t hseed = uint32_t(hh.z) & SEED_MASK;
             const bool kvalid = (uint32_t(hh.z) & KEY_VALID) != 0;
             const bool hud = (uint32_t(hh.z) & UNDRAWN) != 0;   // (a reset then takes the serial path)
@@ -2491,6 +2621,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                     hpy[m] = hpv[m].y;
                 }
             }
+
             if (q < 2) {
                 uint32_t x = q == 0 ? hseed : hkey;
                 const uint32_t koff = q == 0 ? 0u : 397u;
@@ -2501,7 +2632,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 }
             }
             wave_sync();
+            HSTAMP_T(25);
             if constexpr (PLANETS) planet_update<T, S, PMAX, LPE, PPL>(p, hpv, hpx, hpy, q, np, t0, slot_last, hout);
+            HSTAMP_T(26);
             // until the step wave posts (bounded: it always posts; if the
             // bound expires the mask is not trusted -- no stores, no resets --
             // and the launch reports ASTRO_ERR_HELPER_WAIT)
@@ -2510,9 +2643,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 return QuadCounts{};
             }
             asm volatile("" ::: "memory");
-#ifdef ASTRO_STAMPS
-            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[20])::"memory");
-#endif
+            HSTAMP_R(20);
+            HSTAMP_T(27);
             QuadCounts hc{};
             const uint64_t todo0 = bx.todo;
             if (PLANETS && active && !((todo0 >> (lane & ~(LPE - 1))) & 1ull)) {   // a surviving env: its new planets
@@ -2526,6 +2658,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 reinterpret_cast<int2 *>(st.hdr)[2 * i + 1] = make_int2(int(w2), int(w3));   // pending seed
                 if (drew) reinterpret_cast<uint4 *>(st.stream)[i] = cnew;
             }
+            HSTAMP_T(28);
 #ifdef ASTRO_ABLATE_RESETS   // timing ablation only (wrong results): the helpers create no game
             if (false) {
 #else
@@ -2534,6 +2667,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 for (uint64_t todo = todo0; todo;)   // uniform
                     todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, hud, s_chain,
                                                                   s_serial, GlobalSink<T>{st} STAMP_PASS, pre);
+                HSTAMP_T(29);
                 wave_sync();
                 if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
                 if (active && s_serial[e]) {   // uniform over the quad; rare
@@ -2543,8 +2677,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                     restart_env<T, S, PMAX, LPE>(p, st, i, ng, q, GlobalSink<T>{st});
                 }
             }
+            HSTAMP_R(21);
+            HSTAMP_T(30);
 #ifdef ASTRO_STAMPS
-            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[21])::"memory");
             stamp_[22] = __popcll(todo0);
 #endif
             return hc;
@@ -2626,6 +2761,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // planets_only < PMAX, e.g. the 3-planet games of config 3, none does
     // and the float64 fields skip that slot's division)
     const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
+    const int np_uni = wave_uniform_count(np);   // (config 3's 3-planet games: 3)
     const bool live = tick < p.timeout_tick;
     const bool t0 = tick == 0;
     STAMP(1);
@@ -2636,7 +2772,12 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // ---- index the wave's live bullets densely (bullets_begin); their first
     //      two rounds load during the physics below
     const BulletsGlobal<T> bgl{bullets, ships, planets, BC, NN, base};
-    const BulletsIn<T> bin = bullets_begin<T, LPE>(bgl, lane, e, q, nb, np, t0, s_index, s_kept, s_hit, s_serial);
+    // (the helper-less 4-slot pair instance of millions of envs: bullets
+    // loaded in the pass, see bullets_begin; 1M envs 118.8 -> 118.1 us,
+    // profiles/round5/ab_lazy_bullets_1m.jsonl)
+    constexpr bool EAGER_BULLETS = HELP || OPAQUE || LPE != 2 || PMAX > 4;
+    const BulletsIn<T> bin =
+        bullets_begin<T, LPE, QWIN, EAGER_BULLETS>(bgl, lane, e, q, nb, np, t0, s_index, s_kept, s_hit, s_serial);
     const int total = bin.total;
     STAMP(19);
     // key[397] of the next game's seed (first step of a game): a random
@@ -2748,7 +2889,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 gx = sgx;
                 gy = sgy;
             } else {
-                field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
+                field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last, PMAX <= 4 ? np_uni : 0);
             }
 #endif
         }
@@ -2816,8 +2957,8 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     STAMP(3);
     // ---- bullets (core.py:241-251, 264-266, 295-300): collide with the old
     //      bodies, move, cull, compact in place (bullets_rounds)
-    bullets_rounds<T, S, PMAX, LPE, (HELP || OPAQUE) ? 2 : 1>(p, bgl, bin, lane, e, q, nb, sxf, syf, mpxf, mpyf,
-                                                              s_body, s_index, s_kept, s_hit, gp, gs STAMP_PASS);
+    bullets_rounds<T, S, PMAX, LPE, (HELP || OPAQUE) ? 2 : 1, QWIN, EAGER_BULLETS>(
+        p, bgl, bin, lane, e, q, nb, sxf, syf, mpxf, mpyf, s_body, s_index, s_kept, s_hit, gp, gs STAMP_PASS);
     if constexpr (HELP) {   // the helper has its copy of the headers before any is rewritten (HelpBox.seen)
         if (!wait_lds_word(s_box_all[wv].seen)) report_error(st, ASTRO_ERR_HEADER_WAIT, lane);
     }
@@ -3057,7 +3198,7 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
         // array in scratch, and its stores then sat in the same vmcnt queue
         // as the wave's first loads -- the header wait measured them too)
 #pragma unroll
-        for (int k = 0; k < 23; ++k)
+        for (int k = 0; k < NSTAMP; ++k)
             if (hw == (k >= 20)) row[k] = stamp_[k];
     }
 #else
@@ -3119,57 +3260,6 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
 constexpr int RES_QWIN = 256;   // live bullets per LDS index window (a wave holds up to 32 x 32)
 constexpr int RES_WPG = 4;      // waves per workgroup; two workgroups per CU fit the LDS
 
-// One lane's part of its env across the launch (quad/pair layout): the header
-// (every lane of the env), its own ship (lanes q < S), its planet slots
-// q + LPE m, and how far into the env's bullet row the launch has written.
-template <typename T, int S, int PMAX, int LPE>
-struct ResEnv {
-    using V = typename Store<T>::V;
-    int4 h;
-    V sv;
-    T sb;
-    V pv[PMAX / LPE];
-    int hw;   // slots [0, hw) of the env's LDS row were written by this launch (or loaded)
-};
-
-// A reset pass's new game, one per row of the pass (LDS, over the wave's
-// body rows, which are free once the bullet pass is over).
-template <int S, int PMAX>
-struct ResStage {
-    float4 ship[S];
-    float b[4];
-    float4 planet[PMAX];
-    int4 hdr;
-};
-
-// Reset-pass sink: row r of the pass writes its env's new game into stage[r]
-template <typename T, int S, int PMAX>
-struct StageSink {
-    using V = typename Store<T>::V;
-    ResStage<S, PMAX> *stage;
-    __device__ void ship(int s, int, const V &v, T b) const {
-        stage->ship[s] = make_float4(v.x, v.y, v.z, v.w);
-        stage->b[s] = b;
-    }
-    __device__ void planet(int j, int, int, const V &v) const { stage->planet[j] = make_float4(v.x, v.y, v.z, v.w); }
-    __device__ void header(int, const int4 &h) const { stage->hdr = h; }
-    __device__ StageSink for_row(int r) const { return StageSink{stage + r}; }
-};
-
-// Serial-create sink (create_env with NPART = LPE, part = q): the lane's own
-// ship and planet slots go straight into its registers
-template <typename T, int S, int PMAX, int LPE>
-struct RegSink {
-    using V = typename Store<T>::V;
-    ResEnv<T, S, PMAX, LPE> *r;
-    __device__ void ship(int, int, const V &v, T b) const {
-        r->sv = v;
-        r->sb = b;
-    }
-    __device__ void planet(int, int m, int, const V &v) const { r->pv[m] = v; }
-    __device__ void header(int, const int4 &h) const { r->h = h; }
-};
-
 template <int LPE>
 __device__ __forceinline__ int4 group_bcast0(const int4 &v) {   // lane 0 of the env's group to the group
     return make_int4(quad_bcast_i<0, LPE>(v.x), quad_bcast_i<0, LPE>(v.y), quad_bcast_i<0, LPE>(v.z),
@@ -3197,6 +3287,9 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
     float *__restrict__ reward = reward_all + size_t(kt) * NN * S;
     uint8_t *__restrict__ done_out = done_all + size_t(kt) * NN;
     bool f_reset = false, f_coll = false, f_tout = false, need_reset = false;
+#ifdef ASTRO_STAMPS
+    unsigned long long stamp_[NSTAMP] = {};   // (the stamp build's sections; not recorded here)
+#endif
 
     // ---- the state, from registers
     const int4 h = R.h;
@@ -3219,6 +3312,7 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
     const int nb = active ? min(int(uint32_t(h.y) >> 16), p.b_cap) : 0;
     np = np < 1 ? 1 : (np > PMAX ? PMAX : np);
     const bool slot_last = __builtin_amdgcn_readfirstlane(int(__any(np == PMAX))) != 0;
+    const int np_uni = wave_uniform_count(np);
     const bool live = tick < p.timeout_tick;
     const bool t0 = tick == 0;
     const uint32_t fire_word = p.fire_bits[(live ? tick : 0) >> 5];
@@ -3290,7 +3384,7 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
             gx = sgx;
             gy = sgy;
         } else {
-            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last);
+            field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last, PMAX <= 4 ? np_uni : 0);
         }
         const double thr = p.thrust * double(ctl & 1);
         ax = thr * double(ds) + gx;
@@ -3339,7 +3433,7 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
 
     // ---- bullets (core.py:241-251, 264-266, 295-300), in the LDS rows
     bullets_rounds<T, S, PMAX, LPE, 2, RES_QWIN>(p, bm, bin, lane, e, q, nb, sxf, syf, mpxf, mpyf, s_body, s_index,
-                                                 s_kept, s_hit, gp, gs);
+                                                 s_kept, s_hit, gp, gs STAMP_PASS);
     const int wr_in = s_kept[e];
     const int hit_bits = s_hit[e];
     cnt.n_bin += active && q == 0 ? uint32_t(nb) : 0u;
@@ -3446,13 +3540,15 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
     for (uint64_t todo = __ballot(need_reset); todo;) {   // uniform
         const uint64_t before = todo;
         todo = wave_reset_pass<T, S, PMAX, LPE, false, StageSink<T, S, PMAX>>(
-            p, st, todo, lane, i, pend_seed, pend_key, key_valid || p.key_table, undrawn, s_chain, s_serial, ssink);
+            p, st, todo, lane, i, pend_seed, pend_key, key_valid || p.key_table, undrawn, s_chain, s_serial,
+            ssink STAMP_PASS);
         const uint64_t served = before & ~todo;
         wave_sync();
         const int ldr = lane & ~(LPE - 1);
         if (((served >> ldr) & 1ull) && !s_serial[e]) {   // uniform over the env's lanes
             const ResStage<S, PMAX> &g = stage[__popcll(served & ((1ull << ldr) - 1))];
             const int4 nh = g.hdr;
+            if (q == 0) st.stream[4 * size_t(i) + 3] = g.seed;
             const int sq = q < S ? q : 0;
             const float4 shv = g.ship[sq];
             R.sv = V{shv.x, shv.y, shv.z, shv.w};
@@ -3903,7 +3999,11 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         }
 #ifndef ASTRO_NO_RESIDENT   // (A/B builds only: every K-tick rollout on quad_tick's instance)
         if constexpr (std::is_same<T, float>::value) {
-            if (!one && p.b_cap <= RES_BCAP) {   // K ticks with the state on chip
+            // K ticks with the state on chip, while the grid is at most two
+            // waves per SIMD (c3: 7.3 -> 7.0 us per tick; at 1M envs the
+            // quad_tick instance's three waves per SIMD win: 93 vs 99 us,
+            // profiles/round5/ab_early_lazy_1m.jsonl)
+            if (!one && p.b_cap <= RES_BCAP && int64_t(s.n_env) * lpe <= int64_t(64) * ASTRO_HELP_MAX_WAVES) {
                 const int gr = int((int64_t(s.n_env) * lpe + 64 * RES_WPG - 1) / (64 * RES_WPG));
                 if (lpe == 4)
                     hipLaunchKernelGGL((astro_rollout_res_kernel<T, S, PM, 4>), dim3(gr), dim3(64 * RES_WPG), 0,

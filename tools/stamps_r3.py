@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from astro_amd import BatchedEnv, DEFAULT_CONFIG, _lib  # noqa: E402
 
-NSTAMP = 24
+NSTAMP = 32
 SEGS = dict(hdr_wait=(0, 1), bullets_begin=(1, 19), sincos_gravity=(19, 2), ship_collide=(2, 3),
             bodies_lds=(3, 16), rounds_first=(16, 17), rounds_rest=(17, 4), reward_post=(4, 5),
             spawn_ships=(5, 6), planets=(6, 7), hdr_store=(7, 8))
@@ -128,6 +128,29 @@ def main():
             cut = np.percentile(e, 99)
             ends.append(float((R[okr][e >= cut, 22] > 0).mean()))
         out['helper_top1pct_with_resets'] = float(np.mean(ends))
+    # the helper wave's own sections (s_memtime stamps 24-30, shader cycles),
+    # by the number of finished games it re-created
+    if (S[:, 30] > 0).any():
+        hseg = dict(hdr_chains=(24, 25), planet_update=(25, 26), wait_post=(26, 27), survivor_stores=(27, 28),
+                    reset_passes=(28, 29), tail=(29, 30), total=(24, 30))
+        nr = np.minimum(S[:, 22], 2)
+        hout = {}
+        for k, (x, y) in hseg.items():
+            d = (S[:, y] - S[:, x]).astype(np.float64)
+            row = {}
+            for r in (0, 1, 2):
+                ok = (S[:, x] > 0) & (S[:, y] > 0) & (nr == r)
+                if ok.any():
+                    row[str(r)] = round(float(d[ok].mean()), 1)
+            hout[k] = row
+        out['helper_cycles_by_resets'] = hout
+        st0 = []
+        for t in range(a.ticks):
+            R = S[t * nw:(t + 1) * nw]
+            t0 = R[:, 12].min()
+            ok = R[:, 23] > 0
+            st0.append(((R[ok, 23] - t0) / 100.0).mean() if ok.any() else 0.0)
+        out['helper_start_us_mean'] = float(np.mean(st0))
     # what makes a wave slow: its live bullets, games at their first tick,
     # finished games (stamp 15 = resets | t0 << 8 | bullets << 16)
     info = S[:, 15]
