@@ -452,17 +452,6 @@ struct MTStream {
     uint32_t *ring;  // the env's [624] words
 
     __device__ uint32_t next() {
-#ifdef ASTRO_ABLATE_RING   // timing ablation only: the lazy form (wrong past output 226)
-        {
-            const uint32_t x1 = mt_key_next(a, k + 1u);
-            const uint32_t y = (a & 0x80000000u) | (x1 & 0x7fffffffu);
-            const uint32_t z = b ^ (y >> 1) ^ ((x1 & 1u) ? 0x9908b0dfu : 0u);
-            b = mt_key_next(b, k + 1u + MT_PROLOGUE);
-            a = x1;
-            ++k;
-            return mt_temper(z);
-        }
-#endif
         const uint32_t k1 = k + 1u;
         uint32_t x1, nb;
         if (k1 < MT_LAZY) {   // x_{k+1} and x_{k+398} still in the init key: no memory
@@ -1026,9 +1015,6 @@ __device__ __forceinline__ void bullet_pass(const AstroParams &p, typename Store
 #pragma unroll
             for (int s = 0; s < S; ++s) hs[s] = near32(xf, yf, sxf[s], syf[s], gs, amb);
             amb |= t0 & valid;
-#ifdef ASTRO_COLLIDE_F64
-            amb = valid;   // variant: always the exact tests
-#endif
             if (__any(amb)) {   // some lane within 1e-4 of a threshold (or at tick 0): exact tests
                 bool bh64 = false, hs64[S];
 #pragma unroll
@@ -1101,13 +1087,8 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
                                                            int auto_reset) {
     using V = typename Store<T>::V;
     const int N = st.n_env;
-#ifdef ASTRO_ENVS_PER_WAVE   // occupancy experiment: fewer envs per wave
-    const int i = blockIdx.x * ASTRO_ENVS_PER_WAVE + int(threadIdx.x);
-    const bool active = i < N && int(threadIdx.x) < ASTRO_ENVS_PER_WAVE;
-#else
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool active = i < N;
-#endif
     uint32_t n_bin = 0, n_bout = 0, n_pl = 0, n_drop = 0;
     bool f_reset = false, f_coll = false, f_tout = false;
 #ifdef ASTRO_STAMPS
@@ -1236,9 +1217,6 @@ __global__ __launch_bounds__(BLOCK) void astro_step_kernel(AstroParams p, AstroS
             bool hh = false;
             if (S == 2) hh = near32(float(sx[0]), float(sy[0]), float(sx[S - 1]), float(sy[S - 1]), gss, amb);
             amb |= t0;
-#ifdef ASTRO_COLLIDE_F64
-            amb = true;
-#endif
             if (__any(amb)) {   // the exact tests, for the ambiguous lanes (never tick 0, see near32_t0)
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
@@ -1974,10 +1952,6 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
                     ndy = pdy + double(gy * dtf);
                 } else {
                     double gx, gy;
-#ifdef ASTRO_ABLATE_PLANETFIELD   // timing ablation only (wrong results)
-                    gx = px[1] - pxj;
-                    gy = py[1] - pyj;
-#else
                     if constexpr ((LPE == 2 && (PMAX == 4 || PMAX == 8)) || (LPE == 4 && PMAX == 4)) {
                         // field<double> at planet j from the shared factors:
                         // term k = F(j, k) * (p_k - p_j) summed in k order.  The
@@ -2012,7 +1986,6 @@ __device__ __forceinline__ void planet_update(const AstroParams &p, const typena
                     } else {
                         field<double, PMAX>(px, py, np, pxj, pyj, p.gm, gx, gy);
                     }
-#endif
                     ndx = pdx + gx * p.dt;
                     ndy = pdy + gy * p.dt;
                 }
@@ -2224,11 +2197,7 @@ __device__ __forceinline__ BulletsIn<T> bullets_begin(const BM &bm, int lane, in
     BulletsIn<T> b;
     const int incl = wave_incl_scan(q == 0 ? nb : 0, lane);
     b.off = incl - nb;
-#ifdef ASTRO_ABLATE_BULLETS   // timing ablation only (wrong results)
-    b.total = 0;
-#else
     b.total = __builtin_amdgcn_readlane(incl, 63);
-#endif
     b.tag = bw_tag(e, np, t0);
     if (q == 0) {
         s_kept[e] = 0;
@@ -2557,10 +2526,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             // launch's input whatever the memory system's timing (the store
             // depends on the loaded value: it waits for the load's return)
             if (lane == 0) *lds_word(bx.seen) = uint32_t(hh.x) | 1u;
-#ifdef ASTRO_PROBE_IDLE_HELPERS   // measurement build only (wrong results): helpers only handshake
-            if (!wait_lds_word(bx.flag)) report_error(st, ASTRO_ERR_HELPER_WAIT, lane);
-            return QuadCounts{};
-#endif
             const uint32_t hseed = uint32_t(hh.z) & SEED_MASK;
             const bool kvalid = (uint32_t(hh.z) & KEY_VALID) != 0;
             const bool hud = (uint32_t(hh.z) & UNDRAWN) != 0;   // (a reset then takes the serial path)
@@ -2659,11 +2624,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 if (drew) reinterpret_cast<uint4 *>(st.stream)[i] = cnew;
             }
             HSTAMP_T(28);
-#ifdef ASTRO_ABLATE_RESETS   // timing ablation only (wrong results): the helpers create no game
-            if (false) {
-#else
             if (todo0) {   // uniform
-#endif
                 for (uint64_t todo = todo0; todo;)   // uniform
                     todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, hud, s_chain,
                                                                   s_serial, GlobalSink<T>{st} STAMP_PASS, pre);
@@ -2783,21 +2744,15 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // key[397] of the next game's seed (first step of a game): a random
     // gather into the 4 GiB key table, issued after every load the physics
     // waits for, so only its consumers (header store, reset) wait for it
-#ifndef ASTRO_ABLATE_PENDING
     if (!PENDING_ON_HELPER && q == 0 && !key_valid && !undrawn && p.key_table)
         pend_key = p.key_table[pend_seed & SEED_MASK];
-#endif
     // stream cursor, for check_pending (read there under this same condition
     // only).  Every lane loads, the others their own header again (the line
     // just read: no traffic).  A conditional load made the compiler merge
     // its value with the other lanes' zeros right after it, i.e. wait for it
     // -- and for every load before it, the key-table gather included -- at
     // the top of the wave (c3 13.10 -> 12.65 us, c2 6.74 -> 6.64 us, A/B)
-#ifdef ASTRO_ABLATE_PENDING   // timing ablation only (wrong results): the step wave does no pending-seed work
-    const bool want_c = false;
-#else
     const bool want_c = !PENDING_ON_HELPER && q == 0 && (undrawn || (!key_valid && p.key_table && p.planets_only));
-#endif
     uintptr_t c_stream = reinterpret_cast<uintptr_t>(st.stream), c_hdr = reinterpret_cast<uintptr_t>(st.hdr);
     asm volatile("" : "+s"(c_stream), "+s"(c_hdr));   // values, not a select between the fields' addresses
     const uint4 c_pend = load_u4_global(want_c ? c_stream : c_hdr, size_t(i));
@@ -2836,12 +2791,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         }
     }
     float ds, dc;
-#ifdef ASTRO_ABLATE_SINCOS   // timing ablation only (wrong results)
-    ds = float(mb);
-    dc = float(mx);
-#else
     np_sincosf(float(mb), ds, dc);
-#endif
     double ax = 0.0, ay = 0.0;
     // Quad kernel, 4 slots: the ships' float64 fields split over the quad --
     // lane q evaluates ship (q & 1)'s terms of planet slots q >> 1 and
@@ -2881,17 +2831,12 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             gx = double(fx);
             gy = double(fy);
         } else {
-#ifdef ASTRO_ABLATE_SHIPFIELD   // timing ablation only (wrong results)
-            gx = px[0] - mx;
-            gy = py[0] - my;
-#else
             if constexpr (LPE == 4 && PMAX == 4) {
                 gx = sgx;
                 gy = sgy;
             } else {
                 field<double, PMAX>(px, py, np, mx, my, p.gm, gx, gy, slot_last, PMAX <= 4 ? np_uni : 0);
             }
-#endif
         }
         const double thr = p.thrust * double(ctl & 1);
         ax = thr * double(ds) + gx;
@@ -3060,11 +3005,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 if constexpr (PENDING_ON_HELPER) {   // words 2-3: the helper's
                     st_out(&reinterpret_cast<int2 *>(st.hdr)[2 * is], make_int2(tick + 1, np | (fl << 8) | (w << 16)));
                 } else {
-#ifdef ASTRO_ABLATE_PENDING
-                    const uint32_t kv = key_valid ? KEY_VALID : 0u;
-#else
                     const uint32_t kv = check_pending(p, st, is, key_valid, undrawn, c_pend, pend_seed, pend_key);
-#endif
                     st_out(&reinterpret_cast<int4 *>(st.hdr)[is],
                            make_int4(tick + 1, np | (fl << 8) | (w << 16), int(pend_seed | kv), int(pend_key)));
                 }
@@ -4032,12 +3973,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
                                s, drv, r, d, st, ar);
         return launched(lpe == 4 ? "astro_step(quad)" : "astro_step(pair)");
     }
-#ifdef ASTRO_ENVS_PER_WAVE
-    const int grid = (s.n_env + ASTRO_ENVS_PER_WAVE - 1) / ASTRO_ENVS_PER_WAVE;
-    st = nullptr;
-#else
     const int grid = (s.n_env + BLOCK - 1) / BLOCK;
-#endif
     const size_t N = size_t(s.n_env);
     for (int k = 0; k < drv.ticks; ++k) {   // the lane kernel: one launch per tick
         TickDriver one = drv;

@@ -243,12 +243,13 @@ class BatchedEnv:
         reward = torch.empty(k, self.n_env, self.S, dtype=torch.float32, device=self.device)
         done = torch.empty(k, self.n_env, dtype=torch.uint8, device=self.device)
         self.launch_many(c.data_ptr(), k, reward.data_ptr(), done.data_ptr(), auto_reset, stats)
-        if k:
-            self._last = (reward[-1], done[-1])
+        self._last = (reward[-1], done[-1]) if k else None
         return reward, done
 
     def launch_many(self, control_ptr, k, reward_ptr, done_ptr, auto_reset=None, stats=True, stream=None):
-        """Raw astro_step_many (no checks, no allocation): for timed loops."""
+        """Raw astro_step_many (no checks, no allocation): for timed loops.
+        The rewards and dones go to the caller's buffers only, so info()
+        raises until the next step()/step_many()/launch()/rollout()."""
         ar = self.auto_reset if auto_reset is None else bool(auto_reset)
         rc = self.lib.astro_step_many(
             ctypes.byref(self.params), ctypes.byref(self.state), control_ptr, int(k), reward_ptr, done_ptr,
@@ -256,6 +257,7 @@ class BatchedEnv:
             stream if stream is not None else _stream_ptr(self.device))
         if rc != 0:
             _lib.check(rc, 'astro_step_many')
+        self._last = False   # info(): the last tick's reward/done are not held here
 
     def launch(self, control_ptr, auto_reset=None, stats=True, stream=None):
         """Raw launch (no checks, no allocation): for timed loops/graphs."""
@@ -337,7 +339,10 @@ class BatchedEnv:
         a launch reported a device fault (a host synchronisation)."""
         if check:
             self.check_errors()
-        reward, done = getattr(self, '_last', None) or (self.reward, self.done)
+        last = getattr(self, '_last', None)
+        if last is False:
+            raise RuntimeError('info() after a raw launch_many(): its reward/done are in the caller\'s buffers')
+        reward, done = last or (self.reward, self.done)
         hit = ((reward < 0) & (done == 1)[:, None]).to(torch.uint8)
         hit = (hit << torch.arange(self.S, device=self.device, dtype=torch.uint8)[None, :]).sum(1)
         fl = self.flags

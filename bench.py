@@ -134,11 +134,17 @@ def aggregate_roofline(bytes_all_ranks, steps, wall_max, n_dev):
 def add_cpu_baseline(out, wl, args):
     """The CPU baseline fields of the line (rank 0, after the GPU work)."""
     procs = args.cpu_procs or cpu_share()
-    out['cpu_baseline'] = cpu_baseline(wl['cfg'], args.cpu_seconds, procs, wl['planets_only'])
-    out['speedup_vs_cpu'] = out['value'] / out['cpu_baseline']['value'] if out['value'] else None
+    cb = cpu_baseline(wl['cfg'], args.cpu_seconds, procs, wl['planets_only'])
+    world = out.get('ranks', 1)
+    cb['host_share'] = ('rank 0\'s CPU share (%d of the job\'s %d GPU shares)' % (1, world) if world > 1
+                        else 'the one GPU\'s CPU share')
+    out['cpu_baseline'] = cb
+    out['speedup_vs_cpu'] = out['value'] / cb['value'] if out['value'] else None
+    out['speedup_basis'] = ('all %d ranks\' env-steps/s over one host share\'s CPU env-steps/s' % world if world > 1
+                            else 'one GPU over its host share')
 
 
-def single_game_latency(cfg, ticks=2000, seed=0):
+def single_game_latency(cfg, ticks=2000, seed=0, cpu=True):
     """The single-game drop-in (astro_amd.core, what astro/server.py's
     game_tick and core.play's loop call): us per core.step tick with random
     controls, re-creating on termination, and us per tick of core.play with
@@ -155,6 +161,8 @@ def single_game_latency(cfg, ticks=2000, seed=0):
     out['mode'] = default
     core.SHIM_MODE = default
     core._ENVS.clear()
+    if not cpu:
+        return out
     # the CPU comparison for this same path: oracle/port.py's core.step on
     # one host core, the same config, the same loop (controls drawn up front,
     # re-create on termination)
@@ -684,7 +692,7 @@ def main():
         )
         out.update(extras)
         if not args.no_single:   # (rank 0's own GPU; every rank is past the GPU region)
-            out['single_game'] = single_game_latency(DEFAULT_CONFIG)
+            out['single_game'] = single_game_latency(DEFAULT_CONFIG, cpu=not args.no_cpu)
     # rank 0's host-side lines run after every rank has left the GPU region
     # (the last collective above): the CPU baseline of the same workload, on
     # this rank's CPU share, for any number of ranks

@@ -267,7 +267,7 @@ def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap, kernel):
 
 
 @pytest.mark.parametrize('kernel', KERNELS)
-def test_fire_schedule_table_path(kernel):
+def test_irregular_fire_schedule(kernel):
     """A config whose fire schedule is not periodic (reload_time 0.33: the
     host's float64 reload recurrence, core.py:262-280, fires on ticks 1, 2,
     4, 5, ... not every k-th) against the oracle."""
