@@ -3121,8 +3121,13 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 #endif
 constexpr int P8_WAVES = ASTRO_P8_WAVES, P4_WAVES = ASTRO_P4_WAVES, M4_WAVES = ASTRO_M4_WAVES;
 
+// STATS: the one-tick instances come in two builds, with the counters and
+// without (a launch with a null stats pointer): compiled in but switched off
+// at run time they still cost c3 0.6 us per launch, switched on 1.6 us of
+// 12.1 (the per-lane counts, the wave sums and the row atomics at the
+// slowest waves' ends; profiles/round5/ab_stats_flush.jsonl)
 template <typename T, int S, int PMAX, bool MULTI, int LPE, bool BOTS = false, bool HELP = false,
-          int WPG = QW>
+          int WPG = QW, bool STATS = true>
 __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS || PMAX > 4 ? 2 : M4_WAVES) : (PMAX > 4 ? P8_WAVES : P4_WAVES)) void astro_step_quad_kernel(AstroParams p, AstroState st, TickDriver drv,
                                                                 float *__restrict__ reward_all,
                                                                 uint8_t *__restrict__ done_all,
@@ -3163,10 +3168,10 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
             c = quad_tick<T, S, PMAX, LPE, true, BOTS>(a.p, a.st, a.drv, a.reward, a.done, a.stats != nullptr,
                                                         a.auto_reset, kt);
         } else {
-            c = quad_tick<T, S, PMAX, LPE, false, false, HELP, WPG>(p, st, drv, reward_all, done_all, stats != nullptr,
-                                                               auto_reset, kt);
+            c = quad_tick<T, S, PMAX, LPE, false, false, HELP, WPG>(p, st, drv, reward_all, done_all,
+                                                               STATS && stats != nullptr, auto_reset, kt);
         }
-        if (stats) {
+        if (STATS && stats) {
             const int row = __builtin_amdgcn_readfirstlane(int(blockIdx.x * WPG + (threadIdx.x / 64) % WPG));
             if (row * (64 / LPE) < st.n_env)
                 flush_counts(stats + size_t(row) * ASTRO_NSTATS, c, p.b_cap * (64 / LPE) < 65536);
@@ -3925,16 +3930,23 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         // a one-tick launch of at most ASTRO_HELP_MAX_WAVES waves (two per
         // SIMD: c2, c3) gets helper waves for its resets (HelpBox)
         if (one && ar && int64_t(s.n_env) * lpe <= int64_t(64) * ASTRO_HELP_MAX_WAVES) {
-            if (lpe == 4)   // (small N: two step waves per workgroup spread the few waves over more CUs)
-                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, true, QW_SMALL>),
-                                   dim3(int((int64_t(s.n_env) * 4 + 64 * QW_SMALL - 1) / (64 * QW_SMALL))),
-                                   dim3(2 * 64 * QW_SMALL), 0, stream, p, s, drv, r, d, st, ar);
-            else
-            {   // (8 planet slots: four, a 16-wave workgroup would cap the 8-slot code at 128 VGPRs)
+            if (lpe == 4) {   // (small N: two step waves per workgroup spread the few waves over more CUs)
+                const dim3 g(int((int64_t(s.n_env) * 4 + 64 * QW_SMALL - 1) / (64 * QW_SMALL))), b(2 * 64 * QW_SMALL);
+                if (st)
+                    hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, true, QW_SMALL, true>), g, b,
+                                       0, stream, p, s, drv, r, d, st, ar);
+                else
+                    hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, true, QW_SMALL, false>), g,
+                                       b, 0, stream, p, s, drv, r, d, st, ar);
+            } else {   // (8 planet slots: four, a 16-wave workgroup would cap the 8-slot code at 128 VGPRs)
                 constexpr int W = PM > 4 ? 4 : QW_PAIR_HELP;
-                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true, W>),
-                                   dim3(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), dim3(2 * 64 * W), 0,
-                                   stream, p, s, drv, r, d, st, ar);
+                const dim3 g(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), b(2 * 64 * W);
+                if (st)
+                    hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true, W, true>), g, b, 0,
+                                       stream, p, s, drv, r, d, st, ar);
+                else
+                    hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true, W, false>), g, b, 0,
+                                       stream, p, s, drv, r, d, st, ar);
             }
             return launched(lpe == 4 ? "astro_step(quad, helpers)" : "astro_step(pair, helpers)");
         }
@@ -3956,17 +3968,26 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
             }
         }
 #endif
-        if (lpe == 4 && one)
-            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
-                               s, drv, r, d, st, ar);
+        if (lpe == 4 && one) {
+            if (st)
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, false, QW, true>), dim3(grid),
+                                   dim3(QBLOCK), 0, stream, p, s, drv, r, d, st, ar);
+            else
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, false, QW, false>), dim3(grid),
+                                   dim3(QBLOCK), 0, stream, p, s, drv, r, d, st, ar);
+        }
         else if (lpe == 4)
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 4>), dim3(grid), dim3(QBLOCK), 0, stream, p,
                                s, drv, r, d, st, ar);
         else if (one) {
             constexpr int W = PM > 4 ? QW : QW_PAIR;
-            hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, false, W>),
-                               dim3(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), dim3(64 * W), 0, stream, p,
-                               s, drv, r, d, st, ar);
+            const dim3 g(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), b(64 * W);
+            if (st)
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, false, W, true>), g, b, 0, stream,
+                                   p, s, drv, r, d, st, ar);
+            else
+                hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, false, W, false>), g, b, 0,
+                                   stream, p, s, drv, r, d, st, ar);
         }
         else
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 2>), dim3(grid), dim3(QBLOCK), 0, stream, p,

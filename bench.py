@@ -298,6 +298,8 @@ def main():
     ap.add_argument('--steps', type=int, default=1000)
     ap.add_argument('--warmup', type=int, default=50)
     ap.add_argument('--workload', default='c3', choices=sorted(WORKLOADS))
+    ap.add_argument('--counters-in-region', action='store_true',
+                    help='time the launches that count (stats rows) instead of counting in K further launches')
     ap.add_argument('--n-env', type=int, default=0, help='override envs per GPU')
     ap.add_argument('--state', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
@@ -389,10 +391,11 @@ def main():
     # rollout instance (the first launch after the switch is the slow one),
     # then the W warmup launches
     settle = 3
+    cnt = args.counters_in_region   # (the region's launches: the build without the counters, unless asked)
     for t in range(settle):
-        env.launch(ptrs[t % max(1, ticks)])
+        env.launch(ptrs[t % max(1, ticks)], stats=cnt)
     for t in range(args.warmup):
-        env.launch(ptrs[t])
+        env.launch(ptrs[t], stats=cnt)
     barrier()
 
     # Timed region: every one of the K launches has its own control buffer.
@@ -416,7 +419,7 @@ def main():
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cap):
                     for k in range(g0, min(args.steps, g0 + args.graph)):
-                        env.launch(ptrs[args.warmup + k])
+                        env.launch(ptrs[args.warmup + k], stats=cnt)
                 graphs.append(g)
         stream.wait_stream(cap)
         replays = [g.replay for g in graphs]
@@ -467,9 +470,9 @@ def main():
         ev0.record(stream)
     t0 = time.perf_counter()
     if use_c:
-        env.launch_many(ptrs[args.warmup], args.steps, rew_k.data_ptr(), done_k.data_ptr())
+        env.launch_many(ptrs[args.warmup], args.steps, rew_k.data_ptr(), done_k.data_ptr(), stats=cnt)
     for k in range(head):
-        env.launch(ptrs[args.warmup + k])
+        env.launch(ptrs[args.warmup + k], stats=cnt)
     for r in replays:
         r()
     if poll_event:
@@ -509,10 +512,28 @@ def main():
     q0e, q1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     q0e.record(stream)
     for k in range(args.steps):
-        env.launch(ptrs[args.warmup + k])
+        env.launch(ptrs[args.warmup + k], stats=cnt)
     q1e.record(stream)
     torch.cuda.synchronize(dev)
     gpu_ms_per_step = q0e.elapsed_time(q1e) / args.steps
+    # The counters (live bullets and planets for the section 8(d) bytes,
+    # resets, collisions, overflows): K more launches continuing the same
+    # games, of the build that counts (stats row atomics; the timed region's
+    # launches run without them, as a caller that passes no stats buffer
+    # does), timed the same way for the record
+    if not cnt:
+        s0 = env.stat_dict()
+        torch.cuda._sleep(int(2e6 + 4e4 * args.steps))
+        q0e.record(stream)
+        for k in range(args.steps):
+            env.launch(ptrs[args.warmup + k], stats=True)
+        q1e.record(stream)
+        torch.cuda.synchronize(dev)
+        gpu_ms_counting = q0e.elapsed_time(q1e) / args.steps
+        dev_err |= env.device_errors(clear=False)
+        s1 = env.stat_dict() if not dev_err else dict(s0)
+    else:
+        gpu_ms_counting = gpu_ms_per_step
     gpu_timing = ('%d launches issued back to back behind a spin kernel long enough for the host to submit them '
                   'all (right after the timed region, continuing its games): hipEvent pair / %d'
                   % (args.steps, args.steps))
@@ -524,7 +545,7 @@ def main():
     for k in range(args.calib):
         a, b = evs[k]
         a.record(stream)
-        env.launch(ptrs[(args.warmup + k) % ticks])
+        env.launch(ptrs[(args.warmup + k) % ticks], stats=cnt)
         b.record(stream)
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
@@ -671,6 +692,11 @@ def main():
             issue_roofline=issue,
             gpu_ms_per_step=gpu_ms_per_step, gpu_ms_per_step_stream_events=gpu_ms_stream,
             gpu_ms_per_step_graph_replay=gpu_ms_graph,
+            gpu_ms_per_step_counting=gpu_ms_counting,
+            counters=('the timed launches' if cnt else
+                      '%d further launches right after the timed region, continuing its games, of the instance that '
+                      'counts (stats rows; the timed region runs the one without counters, as a caller passing no '
+                      'stats buffer does): the stats below and the section 8(d) bytes per launch' % args.steps),
             timed_region=('%d launches issued from C in one astro_step_many call' % args.steps) if use_c else
                          '%d launches: %d eager, then %s' % (
                 args.steps, head, ('%d hipGraph replay(s) of up to %d launches (%s), each graph replayed once '

@@ -670,6 +670,48 @@ def test_resident_rollout_equals_stepping(kernel, case):
         assert int(((a.flags & 1) != 0).sum()) > 0   # bullets were dropped
 
 
+PLAIN_CASES = {
+    # (kernel, auto_reset, n_env, p_pad, state dtype): every one-tick quad/pair
+    # instance -- with helper waves (auto-reset, <= 2,048 waves) and without
+    'quad_helpers': ('quad', True, 1500, 4, torch.float32),
+    'pair_helpers': ('pair', True, 1500, 4, torch.float32),
+    'pair_helpers_8': ('pair', True, 1500, 8, torch.float32),
+    'pair_helpers_f64': ('pair', True, 1500, 4, torch.float64),
+    'quad_plain': ('quad', False, 1500, 4, torch.float32),
+    'pair_plain_8': ('pair', False, 1500, 8, torch.float32),
+    'pair_large_resets': ('pair', True, 70000, 4, torch.float32),
+    'quad_large_resets': ('quad', True, 40000, 8, torch.float32),
+}
+
+
+@pytest.mark.parametrize('case', sorted(PLAIN_CASES))
+def test_plain_instance_equals_counting(case):
+    """A launch without a stats buffer runs the one-tick instance built
+    without the counters (STATS = false); stepping with it == stepping with
+    the counting instance, bit for bit on every state array, reward and done
+    (the counting instance is the one the oracle tests check)."""
+    from astro_amd import BatchedEnv
+    kernel, ar, n, p_pad, dt = PLAIN_CASES[case]
+    cfg = CFG['rapid'] if p_pad == 4 else CFG['default']._replace(max_planets=8)
+    envs = [BatchedEnv(cfg, n, device='cuda:0', b_cap=24, p_pad=p_pad, dtype=dt, auto_reset=ar, kernel=kernel,
+                       env_offset=5) for _ in range(2)]
+    for e in envs:
+        e.reset()
+        e.rollout(20, 'random', tick0=1 << 21, auto_reset=True)   # games of several ages
+    a, b = envs
+    K = 40
+    ctl = torch.from_numpy(np.random.RandomState(17).randint(0, 6, size=(K, n, a.S)).astype(np.int8)).cuda()
+    n_done = 0
+    for k in range(K):
+        _, ra, da = a.step(ctl[k], stats=True)
+        _, rb, db = b.step(ctl[k], stats=False)
+        assert torch.equal(ra, rb) and torch.equal(da, db), k
+        n_done += int(da.ne(0).sum())
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream', 'stream_ring'):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert n_done > 0
+
+
 @pytest.mark.parametrize('kernel', KERNELS)
 def test_step_many_equals_stepping(kernel):
     """step_many(controls [K, N, S]) (astro_step_many: K one-tick launches

@@ -21,7 +21,7 @@ import bench  # noqa: E402
 from astro_amd import BatchedEnv, DEFAULT_CONFIG, _lib  # noqa: E402
 
 
-def make(spec, wl, n, ticks, rollout):
+def make(spec, wl, n, ticks, rollout, stamp_rows=False):
     lib, _, kernel = spec.partition(':')
     _lib._lib = None
     _lib.load(os.path.join(ROOT, 'astro_amd', lib + '.so'))
@@ -29,6 +29,9 @@ def make(spec, wl, n, ticks, rollout):
     env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=w['b_cap'],
                      p_pad=w['p_pad'], auto_reset=True, kernel=kernel or 'auto', planets_only=w['planets_only'])
     env.reset()
+    if stamp_rows:   # room for a -DASTRO_STAMPS build's per-wave rows (32 int64 per wave)
+        lpe = dict(lane=1, quad=4, pair=2)[env.step_kernel]
+        env.stats = torch.zeros((n * lpe + 63) // 64, 32, dtype=torch.int64, device='cuda:0')
     if rollout > 0:   # age the batch as bench.py does (games of every age, bullets in flight)
         env.rollout(rollout, 'random', tick0=1 << 40, stats=False)
     ctl = torch.from_numpy(bench.controls(0, n, env.S, ticks)).cuda()
@@ -53,6 +56,7 @@ def main():
     ap.add_argument('--n-env', type=int, default=0)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--stamp-rows', action='store_true', help='per-wave stats rows (for -DASTRO_STAMPS builds)')
     ap.add_argument('--burn-in', type=int, default=300, help='random-policy rollout ticks after reset (bench.py: 300)')
     a = ap.parse_args()
     libs = a.libs.split(',')
@@ -61,7 +65,7 @@ def main():
     rolls = {l: [] for l in libs}
     for r in range(a.rounds):
         for lib in libs:
-            env, g = make(lib, a.workload, n, 150, a.burn_in)
+            env, g = make(lib, a.workload, n, 150, a.burn_in, a.stamp_rows)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
