@@ -3134,7 +3134,8 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
                                                                 unsigned long long *stats, int auto_reset) {
 #ifdef ASTRO_STAMPS
     unsigned long long stamp_[NSTAMP] = {};
-    quad_tick<T, S, PMAX, LPE, false, false, HELP, WPG>(p, st, drv, reward_all, done_all, stats != nullptr, auto_reset, 0,
+    quad_tick<T, S, PMAX, LPE, false, false, HELP, WPG>(p, st, drv, reward_all, done_all, STATS && stats != nullptr,
+                                                       auto_reset, 0,
                                                    stamp_);
     STAMP(11);
     if (stats && (threadIdx.x & 63) == 0) {   // a helper wave: slots 20-22 of its step wave's row
@@ -3915,6 +3916,11 @@ template <typename T, int S, int PM>
 int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv, float *r, uint8_t *d,
                 uint64_t *stats, int ar, hipStream_t stream) {
     unsigned long long *st = reinterpret_cast<unsigned long long *>(stats);
+#ifdef ASTRO_STAMPS   // (stamp rows go to `stats`; the one-tick launches stamped are the counter-free ones)
+    const bool count = false;
+#else
+    const bool count = st != nullptr;
+#endif
     const int kind = pick_kernel(p, s.n_env);
     if constexpr (PM <= 8)
     if (kind == ASTRO_KERNEL_QUAD || kind == ASTRO_KERNEL_PAIR) {   // all ticks in one launch
@@ -3932,7 +3938,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         if (one && ar && int64_t(s.n_env) * lpe <= int64_t(64) * ASTRO_HELP_MAX_WAVES) {
             if (lpe == 4) {   // (small N: two step waves per workgroup spread the few waves over more CUs)
                 const dim3 g(int((int64_t(s.n_env) * 4 + 64 * QW_SMALL - 1) / (64 * QW_SMALL))), b(2 * 64 * QW_SMALL);
-                if (st)
+                if (count)
                     hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, true, QW_SMALL, true>), g, b,
                                        0, stream, p, s, drv, r, d, st, ar);
                 else
@@ -3941,7 +3947,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
             } else {   // (8 planet slots: four, a 16-wave workgroup would cap the 8-slot code at 128 VGPRs)
                 constexpr int W = PM > 4 ? 4 : QW_PAIR_HELP;
                 const dim3 g(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), b(2 * 64 * W);
-                if (st)
+                if (count)
                     hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, true, W, true>), g, b, 0,
                                        stream, p, s, drv, r, d, st, ar);
                 else
@@ -3969,7 +3975,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         }
 #endif
         if (lpe == 4 && one) {
-            if (st)
+            if (count)
                 hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 4, false, false, QW, true>), dim3(grid),
                                    dim3(QBLOCK), 0, stream, p, s, drv, r, d, st, ar);
             else
@@ -3982,7 +3988,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         else if (one) {
             constexpr int W = PM > 4 ? QW : QW_PAIR;
             const dim3 g(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), b(64 * W);
-            if (st)
+            if (count)
                 hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, false, W, true>), g, b, 0, stream,
                                    p, s, drv, r, d, st, ar);
             else

@@ -33,6 +33,7 @@ def main():
     ap.add_argument('--b2b', action='store_true',
                     help='the measured launches back to back (one stats buffer each, one sync at the end): '
                          'adds the gap between a launch\'s last wave and the next launch\'s first')
+    ap.add_argument('--timing-only', action='store_true')
     a = ap.parse_args()
     _lib._lib = None
     _lib.load(os.path.join(ROOT, 'astro_amd', a.lib + '.so'))
@@ -52,10 +53,14 @@ def main():
     if a.b2b:
         bufs = [torch.zeros(nw, NSTAMP, dtype=torch.int64, device='cuda') for _ in range(a.ticks)]
         torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         for t in range(a.ticks):
             env.stats = bufs[t]
             env.launch(ctl[5 + t].data_ptr(), stats=True)
+        e1.record()
         torch.cuda.synchronize()
+        b2b_event_us = e0.elapsed_time(e1) * 1e3 / a.ticks
         rows = [b.cpu().numpy().astype(np.int64) for b in bufs]
     else:
         for t in range(a.ticks):
@@ -63,6 +68,9 @@ def main():
             env.launch(ctl[5 + t].data_ptr(), stats=True)
             torch.cuda.synchronize()
             rows.append(env.stats.cpu().numpy().astype(np.int64))
+    if a.timing_only:   # (a build without stamps: the event timing of the same launches only)
+        print(json.dumps(dict(workload=a.workload, lib=a.lib, b2b_event_us=b2b_event_us)), flush=True)
+        return
     S = np.concatenate(rows, 0)
     tot = S[:, 11] - S[:, 0]
     out = dict(workload=a.workload, n=n, kernel=env.step_kernel, waves=nw, wave_cycles_mean=float(tot.mean()))
@@ -94,7 +102,7 @@ def main():
         span = [(last[t] - first[t]) / 100.0 for t in range(a.ticks)]
         gap = [(first[t + 1] - last[t]) / 100.0 for t in range(a.ticks - 1)]
         per = [(first[t + 1] - first[t]) / 100.0 for t in range(a.ticks - 1)]
-        out['b2b'] = dict(span_us_mean=float(np.mean(span)), gap_us_mean=float(np.mean(gap)),
+        out['b2b'] = dict(event_us_per_launch=b2b_event_us, span_us_mean=float(np.mean(span)), gap_us_mean=float(np.mean(gap)),
                           gap_us_min=float(np.min(gap)), period_us_mean=float(np.mean(per)))
     if (S[:, 21] > 0).any():
         he = []
