@@ -21,7 +21,7 @@ import bench  # noqa: E402
 from astro_amd import BatchedEnv, DEFAULT_CONFIG, _lib  # noqa: E402
 
 
-def make(spec, wl, n, ticks, rollout, stamp_rows=False):
+def make(spec, wl, n, ticks, rollout, stamp_rows=False, stats=False):
     lib, _, kernel = spec.partition(':')
     _lib._lib = None
     _lib.load(os.path.join(ROOT, 'astro_amd', lib + '.so'))
@@ -36,14 +36,14 @@ def make(spec, wl, n, ticks, rollout, stamp_rows=False):
         env.rollout(rollout, 'random', tick0=1 << 40, stats=False)
     ctl = torch.from_numpy(bench.controls(0, n, env.S, ticks)).cuda()
     for t in range(50):
-        env.launch(ctl[t].data_ptr())
+        env.launch(ctl[t].data_ptr(), stats=stats)
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
             for t in range(50, 150):
-                env.launch(ctl[t].data_ptr())
+                env.launch(ctl[t].data_ptr(), stats=stats)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     return env, g
@@ -56,6 +56,8 @@ def main():
     ap.add_argument('--n-env', type=int, default=0)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--stats', action='store_true', help='time the counting launches (default: the counter-free '
+                                                         'ones bench.py times)')
     ap.add_argument('--stamp-rows', action='store_true', help='per-wave stats rows (for -DASTRO_STAMPS builds)')
     ap.add_argument('--burn-in', type=int, default=300, help='random-policy rollout ticks after reset (bench.py: 300)')
     a = ap.parse_args()
@@ -65,7 +67,7 @@ def main():
     rolls = {l: [] for l in libs}
     for r in range(a.rounds):
         for lib in libs:
-            env, g = make(lib, a.workload, n, 150, a.burn_in, a.stamp_rows)
+            env, g = make(lib, a.workload, n, 150, a.burn_in, a.stamp_rows, a.stats or a.stamp_rows)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
