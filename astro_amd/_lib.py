@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # (ASTRO_LIB: another build of the same library, e.g. an A/B variant from tools/build_var.sh)
 LIB_PATH = os.environ.get('ASTRO_LIB') or os.path.join(HERE, 'libastro_hip.so')
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 STAT_NAMES = ('bullets_in', 'bullets_out', 'resets', 'collisions', 'timeouts',
               'overflows', 'planets', 'serial_resets')
@@ -115,6 +115,10 @@ class AstroGameTick(ctypes.Structure):
         ('out_nbullets', ctypes.c_int32),
         ('done_out', ctypes.c_int32),
         ('reward_out', ctypes.c_float * 2),
+        ('flag', ctypes.c_void_p),
+        ('flag_dev', ctypes.c_void_p),
+        ('seq', ctypes.c_uint32),
+        ('reserved', ctypes.c_int32),
     ]
 
 

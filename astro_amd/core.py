@@ -116,7 +116,8 @@ class _Shim:
         self.arena = a = _Arena(env.lib, (
             ('hdr', (1, 4), i4), ('ships', (S, 1, 4), f8), ('ships_b', (S, 1), f8), ('planets', (P, 1, 4), f8),
             ('bullets', (1, b_cap, 4), f8), ('control', (1, S), np.int8), ('fire', (2,), i4), ('seed', (1,), np.uint32),
-            ('reward', (1, S), np.float32), ('done', (1,), np.uint8), ('errors', (1,), np.uint32)),
+            ('reward', (1, S), np.float32), ('done', (1,), np.uint8), ('errors', (1,), np.uint32),
+            ('flag', (1,), np.uint32)),
             env.device, self.mode)
         self.in_bytes = a.end('seed')   # hdr .. seed: a tick's input
         self.event = torch.cuda.Event()
@@ -151,6 +152,8 @@ class _Shim:
                 setattr(t, f, a.host + a.layout[f][0])
             t.control_dev, t.fire_dev = a.ptr('control'), a.ptr('fire')
             t.reward_dev, t.done_dev = a.ptr('reward'), a.ptr('done')
+            # the tick's completion word (astro_game_step waits on it)
+            t.flag, t.flag_dev = a.host + a.layout['flag'][0], a.ptr('flag')
             t.in_ = self.inbuf.__array_interface__['data'][0]
             t.out = self.outbuf.__array_interface__['data'][0]
             # the device's current stream when the game was made (the null

@@ -837,6 +837,8 @@ struct TickDriver {
     int64_t env_offset;      // ASTRO_POLICY_RANDOM: global id of env 0
     int32_t bots;            // ASTRO_POLICY_BOTS: ship s's bot = (bots >> 4s) & 15
     double script_r2, script_threshold, ship_thrust, ship_rspeed, bullet_speed, ship_radius;
+    uint32_t *flag;          // astro_game_step: the completion word the one wave stores flag_seq to
+    uint32_t flag_seq;
 };
 
 __device__ __forceinline__ int ship_bot(const TickDriver &d, int s) {
@@ -3181,6 +3183,13 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
         // wave's next tick reads them: vmcnt(0), on this CU's own L1
         if (kt + 1 < n_ticks) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
+    if constexpr (!MULTI && !HELP) {
+        // a single game's tick (astro_game_step: one env, one wave): the
+        // completion word after every store of the wave (a system-scope
+        // release), which the host reads ahead of the stream's completion
+        if (drv.flag != nullptr && (threadIdx.x & 63) == 0)
+            __hip_atomic_store(drv.flag, drv.flag_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 #endif
 }
 
@@ -4124,8 +4133,9 @@ int astro_abi_version(void) { return ASTRO_ABI_VERSION; }
 
 const char *astro_last_error(void) { return g_err; }
 
-int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control, float *reward,
-               uint8_t *done, uint64_t *stats, int32_t auto_reset, void *stream) {
+static int step_checked(const AstroParams *p, const AstroState *s, const int8_t *control, float *reward,
+                        uint8_t *done, uint64_t *stats, int32_t auto_reset, void *stream, uint32_t *flag,
+                        uint32_t flag_seq) {
     int rc = check_params(p);
     if (rc) return rc;
     if ((rc = check_state(s))) return rc;
@@ -4140,7 +4150,14 @@ int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control,
     drv.control = control;
     drv.policy = ASTRO_POLICY_CONTROL;
     drv.ticks = 1;
+    drv.flag = flag;
+    drv.flag_seq = flag_seq;
     return dispatch<StepL>(*p, *s, drv, reward, done, stats, int(auto_reset), reinterpret_cast<hipStream_t>(stream));
+}
+
+int astro_step(const AstroParams *p, const AstroState *s, const int8_t *control, float *reward,
+               uint8_t *done, uint64_t *stats, int32_t auto_reset, void *stream) {
+    return step_checked(p, s, control, reward, done, stats, auto_reset, stream, nullptr, 0);
 }
 
 int astro_step_many(const AstroParams *p, const AstroState *s, const int8_t *control, int32_t k, float *reward,
@@ -4254,6 +4271,9 @@ int astro_host_alloc(uint64_t bytes, void **host, void **device) {
 
 int astro_host_free(void *host) {
     if (!host) return 0;
+    // (a single game's last launch may still be finishing after its
+    // completion word: nothing is freed under a running kernel)
+    (void)hipDeviceSynchronize();
     const hipError_t e = hipHostFree(host);
     return e == hipSuccess ? 0 : fail(-1000 - int(e), "hipHostFree failed: %s", hipGetErrorString(e));
 }
@@ -4331,12 +4351,32 @@ int astro_game_step(AstroGameTick *t) {
     p.timeout_tick = t->timeout_now ? tick : tick + 1;
     p.fire_bits = t->fire_dev;
     hipStream_t stream = reinterpret_cast<hipStream_t>(t->stream);
-    int rc = astro_step(&p, &t->state, t->control_dev, t->reward_dev, t->done_dev, nullptr, 0, stream);
+    // the completion word: only the one-wave quad/pair launch stores it (the
+    // lane kernel and a helper instance never do: the stream's completion then)
+    const bool use_flag = t->flag && t->flag_dev && pick_kernel(p, 1) != ASTRO_KERNEL_LANE;
+    const uint32_t seq = ++t->seq;
+    int rc = step_checked(&p, &t->state, t->control_dev, t->reward_dev, t->done_dev, nullptr, 0, stream,
+                          use_flag ? t->flag_dev : nullptr, seq);
     if (rc) return rc;
-    hipError_t e;
-    while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
+    hipError_t e = hipErrorNotReady;
+    if (use_flag) {
+        // the word, with a look at the stream every 64 reads (a fault ends
+        // the launch without it)
+        const volatile uint32_t *fl = t->flag;
+        for (uint32_t k = 1; *fl != seq; ++k) {
+            if ((k & 63) == 0 && (e = hipStreamQuery(stream)) != hipErrorNotReady) {
+                if (e != hipSuccess || *fl == seq) break;
+                return fail(-95, "astro_game_step: the launch ended without its completion word");
+            }
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        if (e != hipErrorNotReady && e != hipSuccess)
+            return fail(-1000 - int(e), "astro_game_step: %s", hipGetErrorString(e));
+    } else {
+        while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
+        }
+        if (e != hipSuccess) return fail(-1000 - int(e), "astro_game_step: %s", hipGetErrorString(e));
     }
-    if (e != hipSuccess) return fail(-1000 - int(e), "astro_game_step: %s", hipGetErrorString(e));
     if (*t->errors) {
         const uint32_t bits = *t->errors;
         *t->errors = 0;

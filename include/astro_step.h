@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define ASTRO_ABI_VERSION 20
+#define ASTRO_ABI_VERSION 21
 
 /* Physics constants: the reference Config (core.py:20-41) reduced by the
  * host exactly as the reference evaluates it, plus the fire/timeout
@@ -295,6 +295,14 @@ typedef struct AstroGameTick {
     int32_t out_nbullets;
     int32_t done_out;       /* 0 running, 1 ship collision, 2 timeout */
     float reward_out[2];
+    /* completion word in the arena (host and device addresses of one
+     * uint32): the tick's wave stores `seq` there after its last store
+     * (system-scope release), and the call returns once it reads it, ahead
+     * of the stream's own completion; NULL = wait for the stream */
+    uint32_t *flag;
+    uint32_t *flag_dev;
+    uint32_t seq;           /* the call's own counter (astro_game_step increments it) */
+    int32_t reserved;
 } AstroGameTick;
 int astro_game_step(AstroGameTick *t);
 
