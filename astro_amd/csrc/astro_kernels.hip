@@ -795,7 +795,8 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
             stamp_[k == 0 ? 12 : 13] = t_;                                                \
         }                                                                                \
     } while (0)
-constexpr int NSTAMP = 32;   // 0-13 step sections, 14-15 placement, 16-19 reset pass, 20-31 helper wave
+constexpr int NSTAMP = 36;   // 0-13 step sections, 14-15 placement, 16-19 reset pass, 20-31 helper wave,
+                              // 32-35 the helper's last reset pass (its 16-19)
 // helper-wave stamps: s_memrealtime (HSTAMP_R) and s_memtime (HSTAMP_T) into stamp_[k]
 #define HSTAMP_R(k) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_[k])::"memory")
 #define HSTAMP_T(k)                                                                                   \
@@ -2631,6 +2632,12 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                     todo = wave_reset_pass<T, S, PMAX, LPE, true>(p, st, todo, lane, i, hseed, hkey, hk, hud, s_chain,
                                                                   s_serial, GlobalSink<T>{st} STAMP_PASS, pre);
                 HSTAMP_T(29);
+#ifdef ASTRO_STAMPS
+                stamp_[32] = stamp_[16];
+                stamp_[33] = stamp_[17];
+                stamp_[34] = stamp_[18];
+                stamp_[35] = stamp_[19];
+#endif
                 wave_sync();
                 if (stats) hc.c_serial = __popcll(__ballot(active && q == 0 && s_serial[e]));
                 if (active && s_serial[e]) {   // uniform over the quad; rare

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from astro_amd import BatchedEnv, DEFAULT_CONFIG, _lib  # noqa: E402
 
-NSTAMP = 32
+NSTAMP = 36
 SEGS = dict(hdr_wait=(0, 1), bullets_begin=(1, 19), sincos_gravity=(19, 2), ship_collide=(2, 3),
             bodies_lds=(3, 16), rounds_first=(16, 17), rounds_rest=(17, 4), reward_post=(4, 5),
             spawn_ships=(5, 6), planets=(6, 7), hdr_store=(7, 8))
@@ -140,7 +140,9 @@ def main():
     # by the number of finished games it re-created
     if (S[:, 30] > 0).any():
         hseg = dict(hdr_chains=(24, 25), planet_update=(25, 26), wait_post=(26, 27), survivor_stores=(27, 28),
-                    reset_passes=(28, 29), tail=(29, 30), total=(24, 30))
+                    reset_passes=(28, 29), tail=(29, 30), total=(24, 30),
+                    # the last reset pass's sections (wave_reset_pass stamps 16-19, copied to 32-35)
+                    pass_shuffles_temper=(28, 32), pass_draws=(32, 33), pass_create=(33, 34), pass_stores=(34, 35))
         nr = np.minimum(S[:, 22], 2)
         hout = {}
         for k, (x, y) in hseg.items():
