@@ -25,6 +25,14 @@ from .config import (Bodies, Config, DEFAULT_CONFIG, Game, SOLO_CONFIG,  # noqa:
                      SOLO_EASY_CONFIG, State, Tick, generate_configs, nships)
 from .env import BatchedEnv
 
+try:   # core.step's packing around astro_game_step in C (built by __graft_entry__.build)
+    from . import _gamestep
+except ImportError:   # the same tick with the packing in Python (_step_mapped)
+    _gamestep = None
+# ASTRO_SHIM_PY=1: the Python packing even when the helper is built (tests of both)
+if os.environ.get('ASTRO_SHIM_PY') == '1':
+    _gamestep = None
+
 _ENVS = {}
 
 
@@ -162,6 +170,7 @@ class _Shim:
             self.tick = t
             self.tick_ptr = ctypes.addressof(t)
             self.game_step = env.lib.astro_game_step
+            self.game_step_addr = ctypes.cast(self.game_step, ctypes.c_void_p).value
 
     def stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.env.device).cuda_stream)
@@ -249,6 +258,13 @@ def step(state, control, config):
     sh = _shim(config, nb + S)
     with sh.lock:
         if sh.tick is not None:
+            if _gamestep is not None:   # packing, the C call and the next State in C
+                r = _gamestep.step(sh.tick_ptr, sh.game_step_addr, state, c0, c1, config.dt, config.reload_time,
+                                   config.max_time, State, Bodies)
+                if r is not NotImplemented:
+                    if isinstance(r, int):
+                        _lib.check(r, 'astro_game_step')
+                    return r
             return _step_mapped(sh, state, c0, c1, config, S, nb)
         return _step(sh, state, np.array([c0, c1][:S]), config, S, nb)
 

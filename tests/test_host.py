@@ -297,3 +297,70 @@ def test_first_words_and_long_filtered_streams_match_numpy():
             generate_configs_filtered(DEFAULT_CONFIG._replace(seed=int(ss[i])), 3), 300)]
         assert list(got[i]) == want
     assert idx.max() > 1000
+
+
+def test_gamestep_packing_without_gpu():
+    """astro_amd/_gamestep (core.step's packing around astro_game_step, in C)
+    against a stand-in for the tick: it packs the State into the record's
+    input in the shim's order, sets the call's fields from the reference's
+    float64 bookkeeping, and builds the next State from the output with the
+    shim's dtypes (float32 bullets at a game's first tick, float32 planets
+    for a lone planet) -- or (None, int64 reward) on a collision."""
+    import numpy as np
+    from astro_amd import core
+    from astro_amd.config import Bodies, State
+    gs = core._gamestep
+    if gs is None:
+        import __graft_entry__ as g
+        g.build_gamestep()
+        from astro_amd import _gamestep as gs
+    S, P, B = 2, 4, 8
+    t = _lib.AstroGameTick()
+    t.params = _lib.AstroParams(nships=S, solo=0, p_pad=P, max_planets=P, b_cap=B)
+    inbuf, outbuf = np.zeros(5 * S + 4 * P + 4 * B), np.zeros(5 * S + 4 * P + 4 * B)
+    t.in_ = inbuf.__array_interface__['data'][0]
+    t.out = outbuf.__array_interface__['data'][0]
+    seen = {}
+
+    @ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+    def tick(ptr):   # the next state = the input + 1, two bullets fewer
+        r = _lib.AstroGameTick.from_address(ptr)
+        seen.update(np=r.nplanets, nb=r.nbullets, c=(r.control0, r.control1), first=r.first_step, fire=r.fire_now,
+                    timeout=r.timeout_now)
+        n = 5 * S + 4 * (r.nplanets + r.nbullets)
+        outbuf[:n] = inbuf[:n] + 1
+        r.out_nbullets = r.nbullets
+        r.done_out = 0
+        return 0
+    fn = ctypes.cast(tick, ctypes.c_void_p).value
+    f32 = np.float32
+    st = State(Bodies(np.arange(4, dtype=f32).reshape(2, 2), np.zeros((2, 2), f32), np.array([0.5, 1.5], f32)),
+               Bodies(np.ones((1, 2), f32), np.zeros((1, 2), f32), None),
+               Bodies(np.zeros((3, 2), f32), np.full((3, 2), 2, f32), None), 0.0, 0.0)
+    new, rw = gs.step(ctypes.addressof(t), fn, st, 3, 4, 0.01, 0.005, 1.0, State, Bodies)
+    assert seen == dict(np=1, nb=3, c=(3, 4), first=1, fire=1, timeout=0)
+    assert new.ships.x.dtype == np.float64 and np.array_equal(new.ships.x, st.ships.x + 1)
+    assert np.array_equal(new.ships.b, st.ships.b + 1) and new.ships.b.shape == (2,)
+    assert new.planets.x.dtype == np.float32 and new.planets.b is None      # a lone planet stays float32
+    assert new.bullets.x.dtype == np.float32 and new.bullets.x.shape == (3, 2)   # first tick: float32 bullets
+    assert np.array_equal(new.bullets.dx, st.bullets.dx + 1)
+    assert new.reload == 0.0 + 0.01 - 0.005 and new.t == 0.01 and type(new.t) is float
+    assert rw.dtype == np.float32 and not rw.any()
+    # float64 state, two planets: float64 out; a non-contiguous array -> the Python path
+    st2 = new._replace(ships=new.ships._replace(x=np.asfortranarray(np.ones((2, 3)))[:, :2]))
+    assert gs.step(ctypes.addressof(t), fn, st2, 0, 0, 0.01, 0.005, 1.0, State, Bodies) is NotImplemented
+
+    @ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+    def hit(ptr):
+        r = _lib.AstroGameTick.from_address(ptr)
+        r.done_out, r.reward_out[0], r.reward_out[1] = 1, -1.0, 1.0
+        return 0
+    none, rw = gs.step(ctypes.addressof(t), ctypes.cast(hit, ctypes.c_void_p).value, new, 0, 0, 0.01, 0.005, 1.0,
+                       State, Bodies)
+    assert none is None and rw.dtype == np.int64 and list(rw) == [-1, 1]
+
+    @ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+    def bad(ptr):
+        return -90
+    assert gs.step(ctypes.addressof(t), ctypes.cast(bad, ctypes.c_void_p).value, new, 0, 0, 0.01, 0.005, 1.0,
+                   State, Bodies) == -90

@@ -127,18 +127,65 @@ def _roll(state, i):
 # ------------------------------------------------------------------ GPU
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('mode', ['mapped', 'copy'])
+@pytest.mark.parametrize('mode', ['mapped', 'mapped_py', 'copy'])
 def test_config1_trace_through_hip_shim(mode, monkeypatch):
     """BASELINE config 1 through the drop-in surface: astro_amd.core.create /
     step (one float64 env on the HIP kernel) reproduce the reference's
     1000-tick trace bit for bit, re-creates included -- with the game's arena
-    in host-mapped memory (the default) and in device memory with copies."""
+    in host-mapped memory (the default; its packing in C, and in Python) and
+    in device memory with copies."""
     from astro_amd import core
+    if mode == 'mapped_py':
+        monkeypatch.setattr(core, '_gamestep', None)
+    else:
+        assert mode != 'mapped' or core._gamestep is not None, 'astro_amd/_gamestep not built'
+    mode = 'mapped' if mode == 'mapped_py' else mode
     monkeypatch.setattr(core, 'SHIM_MODE', mode)
     monkeypatch.setattr(core, '_ENVS', {})
     _run_config1(lambda: core.create(DEFAULT_CONFIG), lambda s, c: core.step(s, c, DEFAULT_CONFIG))
     sh = next(iter(core._ENVS.values()))
     assert sh.arena.mode == mode
+
+
+@pytest.mark.gpu
+def test_shim_c_packing_equals_python(monkeypatch):
+    """The C packing of a mapped-arena tick (astro_amd/_gamestep) returns what
+    the Python packing returns: the same values, dtypes and shapes of every
+    State array (float32 at a game's first tick and for a lone planet), the
+    same types of reload and t, and the same end-of-game reward (int64 on a
+    collision), over whole games of every planet count."""
+    from astro_amd import core
+    assert core._gamestep is not None, 'astro_amd/_gamestep not built'
+    monkeypatch.setattr(core, 'SHIM_MODE', 'mapped')
+    monkeypatch.setattr(core, '_ENVS', {})
+    gs = core._gamestep
+    rng = np.random.RandomState(7)
+    ends = set()
+    for seed in range(12):
+        cfg = DEFAULT_CONFIG._replace(seed=seed, max_planets=4)
+        s = core.create(cfg)
+        for _ in range(400):
+            c = rng.randint(0, 6, size=2)
+            monkeypatch.setattr(core, '_gamestep', gs)
+            a, ra = core.step(s, c, cfg)
+            monkeypatch.setattr(core, '_gamestep', None)
+            b, rb = core.step(s, c, cfg)
+            assert ra.dtype == rb.dtype and np.array_equal(ra, rb)
+            if a is None or b is None:
+                assert a is None and b is None
+                ends.add(str(ra.dtype))
+                break
+            assert type(a.reload) is type(b.reload) and a.reload == b.reload
+            assert type(a.t) is type(b.t) and a.t == b.t
+            for f in ('ships', 'planets', 'bullets'):
+                for g in ('x', 'dx', 'b'):
+                    x, y = getattr(getattr(a, f), g), getattr(getattr(b, f), g)
+                    if y is None:
+                        assert x is None
+                    else:
+                        assert x.dtype == y.dtype and x.shape == y.shape and np.array_equal(x, y), (f, g)
+            s = a
+    assert ends   # games ended on the way
 
 
 @pytest.mark.gpu
