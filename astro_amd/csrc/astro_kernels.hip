@@ -1630,16 +1630,18 @@ __device__ __forceinline__ typename Store<T>::V create_planet(const AstroParams 
     return v;
 }
 
-// create() of one env spread over a row of 16 lanes, for PMAX <= 7: each
+// create() of one env spread over a row of 16 lanes, for PMAX <= 8: each
 // lane evaluates ONE direction() -- planet u's position angle (u < PMAX),
-// planet u - PMAX's velocity angle, or the inner ship slot's (u = 2 PMAX) --
-// and the results move by shuffles; lane s < S writes ship s, lane j < n
-// planet j (same arithmetic as create_env, bit for bit).  All lanes of the
-// row must be active; `write` gates the stores.
+// planet u - PMAX's velocity angle, or the inner ship slot's (u = 2 PMAX;
+// with 8 planet slots every lane evaluates that one as a second) -- and the
+// results move by shuffles; lane s < S writes ship s, lane j < n planet j
+// (same arithmetic as create_env, bit for bit).  All lanes of the row must
+// be active; `write` gates the stores.
 template <typename T, int S, int PMAX, class Sink>
 __device__ __forceinline__ int create_env_row(const AstroParams &p, const Sink &sink, int ie,
                                               const CreateDraws<S> &d, int u, int row0, bool write) {
-    static_assert(2 * PMAX + 1 <= 16, "one angle per lane of a 16-lane row");
+    static_assert(2 * PMAX <= 16, "one planet angle per lane of a 16-lane row");
+    constexpr bool INNER_LANE = 2 * PMAX + 1 <= 16;   // the inner ship angle on lane 2 PMAX
     using V = typename Store<T>::V;
     int n = d.n;
     const double stp = TWO_PI / double(n);
@@ -1648,10 +1650,16 @@ __device__ __forceinline__ int create_env_row(const AstroParams &p, const Sink &
     const int j = u < PMAX ? u : (u < 2 * PMAX ? u - PMAX : 0);
     const double orient = base + double(j) * stp;
     float ang = u < PMAX ? float(orient) : float(orient + turn);
-    ang = u == 2 * PMAX ? float(TWO_PI * d.u_inner) : ang;
+    if (INNER_LANE) ang = u == 2 * PMAX ? float(TWO_PI * d.u_inner) : ang;
     float sn, cs;
     np_sincosf(ang, sn, cs);
-    const float is = row_bcast<2 * PMAX>(sn), ic = row_bcast<2 * PMAX>(cs);
+    float is, ic;
+    if constexpr (INNER_LANE) {
+        is = row_bcast<INNER_LANE ? 2 * PMAX : 0>(sn);
+        ic = row_bcast<INNER_LANE ? 2 * PMAX : 0>(cs);
+    } else {
+        np_sincosf(float(TWO_PI * d.u_inner), is, ic);
+    }
     const float vs = row_from<PMAX>(sn), vc = row_from<PMAX>(cs);   // (lanes u < PMAX: lane PMAX + u's)
 
     // ships (core.py:93-109): lane u < S writes ship u
@@ -1767,7 +1775,7 @@ __device__ __forceinline__ uint64_t wave_reset_pass(const AstroParams &p, const 
 
     const Sink sink = sink_all.for_row(row);   // where row `row`'s game goes
     int n, cf = 0;
-    if constexpr (2 * PMAX + 1 <= 16) {
+    if constexpr (2 * PMAX <= 16) {
         n = create_env_row<T, S, PMAX>(p, sink, ie, d, u, row0, on && fast);
     } else {
         if (on && fast) n = create_env<T, S, PMAX, 16, Sink>(p, sink, ie, d, cf, u);
@@ -3118,6 +3126,9 @@ typedef const __attribute__((address_space(4))) QuadArgs *KernArgs;
 // VGPRs; at 2 the 1M-env rollouts ran 110 vs 91 us per tick,
 // profiles/round4/ab_packed_bullets_v1.jsonl), 8 slots and the ScriptBot
 // instance at 2 (at 3 they spill 25 / 55 VGPRs).
+// The 4-slot instances with helper waves share the bound: at 4 waves per
+// SIMD the quad helper instance holds 109-111 VGPRs and the pair one 121-123,
+// no scratch in either (-Rpass-analysis=kernel-resource-usage, round 5).
 // (-DASTRO_P4_WAVES / _P8_WAVES / _M4_WAVES: occupancy A/B builds only)
 #ifndef ASTRO_P8_WAVES
 #define ASTRO_P8_WAVES 3
