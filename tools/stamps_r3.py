@@ -170,6 +170,15 @@ def main():
     out['slow5'] = dict(cycles=float(cyc[slow].mean()), bullets=float(nbul[slow].mean()), t0=float(nt0[slow].mean()),
                         resets=float(nres[slow].mean()), start_us=float(np.concatenate(st)[slow].mean()))
     out['all'] = dict(cycles=float(cyc.mean()), bullets=float(nbul.mean()), t0=float(nt0.mean()), resets=float(nres.mean()))
+    # a step wave's own (last) reset pass (no helper waves): stamps 16-19 are
+    # the pass's there (they overwrite the bullet pass's 16, 17 and 19)
+    rs = (nres > 0) & (S[:, 16] > 0) & (S[:, 19] > 0)
+    if rs.any() and not (S[:, 30] > 0).any():
+        st_pass = np.maximum(S[:, 8], S[:, 9])
+        out['step_pass_cycles'] = dict(
+            waves=int(rs.sum()), before_draws=float((S[rs, 16] - st_pass[rs]).mean()),
+            draws=float((S[rs, 17] - S[rs, 16]).mean()), create=float((S[rs, 18] - S[rs, 17]).mean()),
+            stores=float((S[rs, 19] - S[rs, 18]).mean()), after=float((S[rs, 10] - S[rs, 19]).mean()))
     A = np.stack([np.ones_like(cyc), nbul, nt0, nres], 1).astype(np.float64)
     coef = np.linalg.lstsq(A, cyc, rcond=None)[0]
     out['fit_cycles'] = dict(base=float(coef[0]), per_bullet=float(coef[1]), per_t0=float(coef[2]), per_reset=float(coef[3]))
