@@ -22,10 +22,16 @@ def main():
     ap.add_argument('--ticks', type=int, default=100)
     ap.add_argument('--launches', type=int, default=10)
     ap.add_argument('--burn-in', type=int, default=300)
+    ap.add_argument('--b-cap', type=int, default=0, help='override the workload\'s bullet capacity')
+    ap.add_argument('--lib', default='', help='a library variant under astro_amd/ (A/B builds)')
     a = ap.parse_args()
+    if a.lib:
+        from astro_amd import _lib
+        _lib._lib = None
+        _lib.load(os.path.join(ROOT, 'astro_amd', a.lib + '.so'))
     w = bench.WORKLOADS[a.workload]
     n = a.n_env or w['n']
-    env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=w['b_cap'], p_pad=w['p_pad'],
+    env = BatchedEnv(DEFAULT_CONFIG._replace(**w['cfg']), n, device='cuda:0', b_cap=a.b_cap or w['b_cap'], p_pad=w['p_pad'],
                      auto_reset=True, planets_only=w['planets_only'])
     env.reset()
     env.rollout(a.burn_in, 'random', tick0=1 << 40, stats=False)
