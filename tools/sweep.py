@@ -236,7 +236,7 @@ def main():
             run(lib + ':c2_noreset', D._replace(reload_time=1000), 65536, auto_reset=False)
             run(lib + ':c3_262k', D, 262144)
         return
-    if a.set == 'timing':   # plain timings of alternative builds (e.g. -DASTRO_ABLATE_* ablations)
+    if a.set == 'timing':   # plain timings of alternative builds (-D A/B variants)
         for lib in a.libs.split(','):
             use_lib(lib + '.so')
             run(lib + ':c3', D, 65536)
