@@ -681,6 +681,7 @@ PLAIN_CASES = {
     'pair_plain_8': ('pair', False, 1500, 8, torch.float32),
     'pair_large_resets': ('pair', True, 70000, 4, torch.float32),
     'quad_large_resets': ('quad', True, 40000, 8, torch.float32),
+    'pair_large_8_resets': ('pair', True, 70000, 8, torch.float32),   # config 5's instance
 }
 
 
