@@ -9,9 +9,14 @@ the reference bit for bit (tests/test_gpu_parity.py): inputs are never
 mutated, a finished game returns ``(None, reward)`` with an int64 reward for
 a collision and a float32 reward for a timeout.
 
-This path is latency-bound by design: a tick is one H2D copy of the packed
-state, one tiny launch, one D2H copy and a busy-polled event (``_Shim``);
-bulk simulation belongs on :class:`astro_amd.env.BatchedEnv`.
+This path is latency-bound by design: by default (``ASTRO_SHIM=mapped``) the
+game lives in host-mapped memory the kernel addresses directly and a tick is
+one ``astro_game_step`` C call -- the State packed (in C, ``_gamestep``), one
+one-wave launch on the caller's current stream, a busy-wait on the
+completion word the wave stores after its last store, the next State built
+(~18.7 us per core.step on MI355X); ``ASTRO_SHIM=copy``
+moves a packed device arena with one H2D and one D2H copy per tick.  Bulk
+simulation belongs on :class:`astro_amd.env.BatchedEnv`.
 """
 import ctypes
 import os
@@ -33,7 +38,37 @@ except ImportError:   # the same tick with the packing in Python (_step_mapped)
 if os.environ.get('ASTRO_SHIM_PY') == '1':
     _gamestep = None
 
-_ENVS = {}
+class _ShimCache(dict):
+    """(config without seed, device) -> _Shim.  Emptying it also drops the
+    per-tick fast path (_LAST), so a cleared shim is never used again."""
+
+    def clear(self):
+        global _LAST
+        _LAST = (None, None, None, None)
+        super().clear()
+
+    def __delitem__(self, key):
+        global _LAST
+        _LAST = (None, None, None, None)
+        super().__delitem__(key)
+
+    def pop(self, *a):
+        global _LAST
+        _LAST = (None, None, None, None)
+        return super().pop(*a)
+
+    def popitem(self):
+        global _LAST
+        _LAST = (None, None, None, None)
+        return super().popitem()
+
+
+_ENVS = _ShimCache()
+
+
+def clear_shims():
+    """Drop every single-game shim (their arenas are freed with them)."""
+    _ENVS.clear()
 
 
 def _device():
@@ -95,10 +130,11 @@ class _Arena:
 
 
 # The single-game arena: 'mapped' (default) = the game's arrays in host
-# memory the kernel addresses directly, a tick is one launch and one event;
-# ASTRO_SHIM=copy = a device arena with one packed H2D and one packed D2H copy
-# per tick.  Measured on MI355X (bench.py `single_game`): mapped 35-40 us per
-# core.step, copy 43-53 us
+# memory the kernel addresses directly, a tick is one astro_game_step call
+# (launch + completion-word wait); ASTRO_SHIM=copy = a device arena with one
+# packed H2D and one packed D2H copy per tick.  Measured on MI355X (bench.py
+# `single_game`, round 5): mapped 18.7 us per core.step, copy 38 us (DESIGN.md
+# section 10)
 SHIM_MODE = os.environ.get('ASTRO_SHIM', 'mapped')
 # the step kernel of the one-env game (every kernel gives the same results)
 SHIM_KERNEL = os.environ.get('ASTRO_SHIM_KERNEL', 'auto')
@@ -164,9 +200,9 @@ class _Shim:
             t.flag, t.flag_dev = a.host + a.layout['flag'][0], a.ptr('flag')
             t.in_ = self.inbuf.__array_interface__['data'][0]
             t.out = self.outbuf.__array_interface__['data'][0]
-            # the device's current stream when the game was made (the null
-            # stream by default: the lowest-latency submission measured)
-            t.stream = torch.cuda.current_stream(env.device).cuda_stream
+            # the caller's current stream, refreshed on every tick (step)
+            self.dev_index = env.device.index if env.device.index is not None else torch.cuda.current_device()
+            t.stream = torch._C._cuda_getCurrentRawStream(self.dev_index)
             self.tick = t
             self.tick_ptr = ctypes.addressof(t)
             self.game_step = env.lib.astro_game_step
@@ -211,6 +247,9 @@ class _Shim:
 # the per-tick fast path (one tuple, read and replaced whole: thread-safe)
 _LAST = (None, None, None, None)
 _SHIM_LOCK = threading.Lock()
+
+
+_raw_stream = torch._C._cuda_getCurrentRawStream   # (device index -> hipStream_t, ~0.1 us)
 
 
 def _shim(config, bullets_needed):
@@ -258,6 +297,8 @@ def step(state, control, config):
     sh = _shim(config, nb + S)
     with sh.lock:
         if sh.tick is not None:
+            # (each tick on the caller's current stream, as BatchedEnv's calls)
+            sh.tick.stream = _raw_stream(sh.dev_index)
             if _gamestep is not None:   # packing, the C call and the next State in C
                 r = _gamestep.step(sh.tick_ptr, sh.game_step_addr, state, c0, c1, config.dt, config.reload_time,
                                    config.max_time, State, Bodies)

@@ -3168,6 +3168,10 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
         for (int k = 0; k < NSTAMP; ++k)
             if (hw == (k >= 20)) row[k] = stamp_[k];
     }
+    if constexpr (!MULTI && !HELP) {   // (astro_game_step's completion word, as below)
+        if (drv.flag != nullptr && (threadIdx.x & 63) == 0)
+            __hip_atomic_store(drv.flag, drv.flag_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 #else
     // ---- the launch's ticks: each wave steps its 16 envs on its own, no
     //      grid-wide barrier between ticks (envs never interact); the

@@ -154,13 +154,13 @@ def single_game_latency(cfg, ticks=2000, seed=0, cpu=True):
     default = core.SHIM_MODE
     out = {}
     for mode in sorted(('mapped', 'copy'), key=lambda m: m == default):   # (the default last)
-        core._ENVS.clear()
+        core.clear_shims()
         core.SHIM_MODE = mode
         out.update(_single_game(core, cfg, ticks, seed))
         out['us_per_step_' + mode] = out['us_per_step']
     out['mode'] = default
     core.SHIM_MODE = default
-    core._ENVS.clear()
+    core.clear_shims()
     if not cpu:
         return out
     # the CPU comparison for this same path: oracle/port.py's core.step on
@@ -213,6 +213,49 @@ def _single_game(core, cfg, ticks, seed):
                      'launch, busy-wait, unpack in C); "copy": one H2D copy of the packed state, one launch, one D2H '
                      'copy, one event; the CPU reference port (oracle/port.py) per tick on one core beside it, the '
                      'same loop (controls drawn up front, re-create on termination)')
+
+
+def region_breakdown(stamps, gpu_ms_stream, gpu_ms_per_step, steps):
+    """Where the timed region's wall time went: the host timestamps
+    (submitted = the launches or graph replays handed to the runtime,
+    end_seen = the event behind them seen complete, synchronized = the
+    clock's stop), the GPU's span of the region by the event pair around it
+    (ev0 is recorded just before the clock starts, ev1 behind the launches),
+    and the K launches' own back-to-back GPU time; the differences name the
+    idle GPU time inside the region (first dispatch after the submission,
+    graph overhead) and the host's tail (end poll, synchronize)."""
+    out = {k: v for k, v in stamps.items()}
+    kern = gpu_ms_per_step * steps * 1e3
+    out['kernels_back_to_back'] = kern
+    if gpu_ms_stream is not None:
+        span = gpu_ms_stream * steps * 1e3
+        out['gpu_span_events'] = span
+        out['gpu_idle_in_span'] = span - kern
+        out['host_after_gpu_span'] = stamps['synchronized'] - span
+    out['wall_minus_kernels_per_step'] = (stamps['synchronized'] - kern) / steps
+    return out
+
+
+def counting_pass(env, launch, steps, s0, s1, dev_err, gpu_ms_per_step):
+    """The K launches of the counting instance after the timed region
+    (launch(k) issues the k-th): (s0, s1, gpu ms per launch, error bits).
+    With device error bits already set (dev_err) nothing is launched and
+    stat_dict(), which raises on them, is not called: the line still prints
+    and reports the bits (device_errors), with the region's own s0/s1 and
+    the counter-free GPU time standing in."""
+    if dev_err:
+        return s0, s1, gpu_ms_per_step, dev_err
+    s0 = env.stat_dict()
+    torch.cuda._sleep(int(2e6 + 4e4 * steps))
+    q0e, q1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    q0e.record()
+    for k in range(steps):
+        launch(k)
+    q1e.record()
+    torch.cuda.synchronize(env.device)
+    dev_err |= env.device_errors(clear=False)
+    s1 = env.stat_dict() if not dev_err else dict(s0)
+    return s0, s1, q0e.elapsed_time(q1e) / steps, dev_err
 
 
 def _free_port():
@@ -475,15 +518,22 @@ def main():
         env.launch(ptrs[args.warmup + k], stats=cnt)
     for r in replays:
         r()
+    t_sub = time.perf_counter()
     if poll_event:
         ev1.record(stream)
+        t_rec = time.perf_counter()
         while not ev1.query():   # (busy-poll the end: a blocking wait wakes ~10 us late)
             pass
     else:
+        t_rec = t_sub
         while not stream.query():
             pass
+    t_end = time.perf_counter()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    # host timestamps inside the region (us from the clock's start)
+    stamps = dict(submitted=(t_sub - t0) * 1e6, end_event_recorded=(t_rec - t0) * 1e6,
+                  end_seen=(t_end - t0) * 1e6, synchronized=wall * 1e6)
     # faults of the timed region (read before stat_dict, which raises on them)
     dev_err = env.device_errors(clear=False)
     barrier()
@@ -518,20 +568,13 @@ def main():
     gpu_ms_per_step = q0e.elapsed_time(q1e) / args.steps
     # The counters (live bullets and planets for the section 8(d) bytes,
     # resets, collisions, overflows): K more launches continuing the same
-    # games, of the build that counts (stats row atomics; the timed region's
+    # games, of the build that counts (stats rows; the timed region's
     # launches run without them, as a caller that passes no stats buffer
     # does), timed the same way for the record
     if not cnt:
-        s0 = env.stat_dict()
-        torch.cuda._sleep(int(2e6 + 4e4 * args.steps))
-        q0e.record(stream)
-        for k in range(args.steps):
-            env.launch(ptrs[args.warmup + k], stats=True)
-        q1e.record(stream)
-        torch.cuda.synchronize(dev)
-        gpu_ms_counting = q0e.elapsed_time(q1e) / args.steps
-        dev_err |= env.device_errors(clear=False)
-        s1 = env.stat_dict() if not dev_err else dict(s0)
+        s0, s1, gpu_ms_counting, dev_err = counting_pass(
+            env, lambda k: env.launch(ptrs[args.warmup + k], stats=True), args.steps, s0, s1,
+            dev_err | env.device_errors(clear=False), gpu_ms_per_step)
     else:
         gpu_ms_counting = gpu_ms_per_step
     gpu_timing = ('%d launches issued back to back behind a spin kernel long enough for the host to submit them '
@@ -690,6 +733,7 @@ def main():
                           lanes_per_env=dict(lane=1, quad=4, pair=2)[env.step_kernel],
                           timing=gpu_timing),
             issue_roofline=issue,
+            region_host_us=region_breakdown(stamps, gpu_ms_stream, gpu_ms_per_step, args.steps),
             gpu_ms_per_step=gpu_ms_per_step, gpu_ms_per_step_stream_events=gpu_ms_stream,
             gpu_ms_per_step_graph_replay=gpu_ms_graph,
             gpu_ms_per_step_counting=gpu_ms_counting,

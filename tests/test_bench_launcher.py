@@ -65,3 +65,23 @@ def test_failing_rank_ends_the_launch():
     p, lines = _run(['--gpus', '2', '--stub', '--no-cpu'], {'ASTRO_DIST_BACKEND': 'no-such-backend'})
     assert p.returncode != 0
     assert lines == []
+
+
+def test_counting_pass_skipped_on_device_errors():
+    """With device error bits set by the timed region, bench.py's counting
+    pass launches nothing and does not call stat_dict() (which raises on
+    those bits), so the line still prints and reports them."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class FakeEnv:
+        def stat_dict(self):
+            raise AssertionError('stat_dict() called with device error bits set')
+
+        def device_errors(self, clear=True):
+            raise AssertionError('not expected')
+
+    launched = []
+    s0, s1 = {'resets': 1}, {'resets': 5}
+    out = bench.counting_pass(FakeEnv(), launched.append, 20, s0, s1, 0x4, 0.0101)
+    assert out == (s0, s1, 0.0101, 0x4) and launched == []

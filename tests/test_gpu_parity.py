@@ -20,6 +20,10 @@ CFG = gio.configs()
 
 
 KERNELS = ['lane', 'quad', 'pair']
+# True: the one-tick instances that count (stats rows); False: the same
+# instances built without the counters -- what a caller passing no stats
+# buffer runs, and what bench.py times and the single-game shim runs
+STATS = [False, True]
 
 
 def _env(cfg, n, dtype=torch.float64, b_cap=64, p_pad=8, auto_reset=False, kernel='auto'):
@@ -88,9 +92,10 @@ def test_seed_streams_follow_generate_configs():
         assert (env.game_seed.cpu().numpy().view(np.uint32) == want[:, k]).all()
 
 
+@pytest.mark.parametrize('stats', STATS)
 @pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('fast_end', [False, True])
-def test_planets_only_streams(kernel, fast_end):
+def test_planets_only_streams(kernel, fast_end, stats):
     """planets_only=3 (BASELINE.json's "3 planets" workloads): every game an
     env plays, through reset() and auto-reset alike, is the next seed of its
     generate_configs stream whose create() draws 3 planets, and the game is
@@ -119,16 +124,18 @@ def test_planets_only_streams(kernel, fast_end):
             fresh = batched.create(seeds[fin, games[fin]], P, p_pad=env.p_pad, b_cap=32, store='f32')
             want.put(fin, fresh)
             games[fin] += 1
-        _, rew, done = env.step(torch.from_numpy(ctl).cuda())
+        _, rew, done = env.step(torch.from_numpy(ctl).cuda(), stats=stats)
         assert (done.cpu().numpy() == wdone).all(), t
+        assert np.array_equal(rew.cpu().numpy(), wrew), t
         got = _host_batch(env)
         _assert_same('planets_only t=%d' % t, got, want, np.ones(n, bool), rounding=True)
         assert (env.game_seed.cpu().numpy().view(np.uint32) == seeds[np.arange(n), games - 1]).all(), t
     assert games.max() > 2
 
 
+@pytest.mark.parametrize('stats', STATS)
 @pytest.mark.parametrize('kernel', KERNELS)
-def test_config2_exact_vs_oracle(kernel):
+def test_config2_exact_vs_oracle(kernel, stats):
     """BASELINE.json config 2 as bench.py runs it: 4,096 envs,
     DEFAULT_CONFIG with reload_time=1000 (no bullets), 2 ships, games
     filtered to 3 planets, auto-reset -- 200 ticks, every tick equal to the
@@ -152,20 +159,25 @@ def test_config2_exact_vs_oracle(kernel):
         if fin.size:
             want.put(fin, batched.create(seeds[fin, games[fin]], P, p_pad=env.p_pad, b_cap=32, store='f32'))
             games[fin] += 1
-        _, rew, done = env.step(torch.from_numpy(ctl).cuda())
+        _, rew, done = env.step(torch.from_numpy(ctl).cuda(), stats=stats)
         assert (done.cpu().numpy() == wdone).all(), t
         assert np.array_equal(rew.cpu().numpy(), wrew), t
         _assert_same('c2 t=%d' % t, _host_batch(env), want, np.ones(n, bool), rounding=True)
+    assert games.max() > 1
     st = env.stat_dict()
-    assert st['bullets_in'] == 0 and st['resets'] == int((games - 1).sum()) > 0
+    if stats:
+        assert st['bullets_in'] == 0 and st['resets'] == int((games - 1).sum()) > 0
+    else:   # (the counter-free instance leaves the stats rows alone)
+        assert not any(st.values())
 
 
 # ------------------------------------------------- teacher-forced transitions
 
+@pytest.mark.parametrize('stats', STATS)
 @pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
 @pytest.mark.parametrize('fname', ['steps.npz', 'edge_steps.npz'])
-def test_step_teacher_forced_vs_reference(fname, dtype, kernel):
+def test_step_teacher_forced_vs_reference(fname, dtype, kernel, stats):
     tr = gio.Transitions(fname)
     for name, idx in tr.groups():
         cfg = CFG[name]
@@ -175,7 +187,7 @@ def test_step_teacher_forced_vs_reference(fname, dtype, kernel):
         env = _env(cfg, idx.size, dtype=dtype, b_cap=bcap, kernel=kernel)
         env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
         ctl = tr.z['control'][idx, :S].astype(np.int8)
-        _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+        _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False, stats=stats)
         E, erew, edone = tr.expected(idx, S, b_cap=bcap)
         done = done.cpu().numpy()
         assert (done == edone).all(), name
@@ -255,15 +267,17 @@ def test_whole_games_float64_bit_exact(kernel):
 
 # ----------------------------------------- batched run vs oracle, auto-reset
 
+@pytest.mark.parametrize('stats', STATS)
 @pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('name,n,ticks,bcap', [('default', 4096, 60, 32), ('mp8', 2000, 40, 32),
                                               ('rapid', 517, 30, 6), ('solo', 701, 40, 32),
                                               ('rapid', 77, 70, 100)])
-def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap, kernel):
+def test_batched_auto_reset_vs_oracle(name, n, ticks, bcap, kernel, stats):
     """N envs with auto-reset, float32 state: every tick equals the oracle
     stepped from the kernel's own input state, resets draw the right seeds
-    and create the right games, overflow (small b_cap) is counted alike."""
-    _auto_reset_vs_oracle(CFG[name], name, n, ticks, bcap, kernel)
+    and create the right games, overflow (small b_cap) is counted alike.
+    stats=False: the counter-free build, the one bench.py times."""
+    _auto_reset_vs_oracle(CFG[name], name, n, ticks, bcap, kernel, stats)
 
 
 @pytest.mark.parametrize('kernel', KERNELS)
@@ -278,7 +292,7 @@ def test_irregular_fire_schedule(kernel):
     _auto_reset_vs_oracle(cfg, 'reload0.33', 600, 60, 32, kernel)
 
 
-def _auto_reset_vs_oracle(cfg, name, n, ticks, bcap, kernel):
+def _auto_reset_vs_oracle(cfg, name, n, ticks, bcap, kernel, stats=True):
     P = batched.make_params(cfg)
     env = _env(cfg, n, dtype=torch.float32, b_cap=bcap, auto_reset=True, kernel=kernel)
     env.reset()
@@ -286,6 +300,7 @@ def _auto_reset_vs_oracle(cfg, name, n, ticks, bcap, kernel):
     games = np.ones(n, np.int64)          # game 0 was created by reset()
     rng = np.random.RandomState(1)
     max_wave_bullets = 0   # live bullets of 16 consecutive envs (a quad-kernel wave) at a step's start
+    saw_overflow = False
     for t in range(ticks):
         B = _host_batch(env)
         ctl = rng.randint(0, 6, size=(n, env.S)).astype(np.int8)
@@ -295,19 +310,24 @@ def _auto_reset_vs_oracle(cfg, name, n, ticks, bcap, kernel):
             fresh = batched.create(seeds[fin, games[fin]], P, p_pad=env.p_pad, b_cap=bcap, store='f32')
             want.put(fin, fresh)
             games[fin] += 1
-        _, rew, done = env.step(torch.from_numpy(ctl).cuda())
+        _, rew, done = env.step(torch.from_numpy(ctl).cuda(), stats=stats)
         done = done.cpu().numpy()
         assert (done == wdone).all(), t
         assert np.array_equal(rew.cpu().numpy(), wrew), t
         got = _host_batch(env)
         _assert_same('%s t=%d' % (name, t), got, want, np.ones(n, bool), rounding=True)
         assert (got.overflow == want.overflow).all(), t
+        saw_overflow |= bool(want.overflow.any())
         nb16 = np.pad(B.nbullets, (0, -n % 16)).reshape(-1, 16).sum(1)
         max_wave_bullets = max(max_wave_bullets, int(nb16.max()))
+    assert games.max() > 1
     st = env.stat_dict()
-    assert st['resets'] == int((games - 1).sum())
+    if stats:
+        assert st['resets'] == int((games - 1).sum())
+    else:   # (the counter-free instance leaves the stats rows alone)
+        assert not any(st.values())
     if name == 'rapid' and bcap < 10:
-        assert st['overflows'] > 0
+        assert saw_overflow and (st['overflows'] > 0 or not stats)
     if bcap > 64:   # the quad kernel indexes a wave's bullets in windows of 1024
         assert max_wave_bullets > 1024
 
@@ -471,9 +491,10 @@ def test_config5_full_size_instances_agree():
         assert torch.equal(getattr(lane, f), getattr(full, f)), f
 
 
+@pytest.mark.parametrize('stats', STATS)
 @pytest.mark.parametrize('kernel', KERNELS)
 @pytest.mark.parametrize('tick', [0, 7])
-def test_near_threshold_collisions_exact(tick, kernel):
+def test_near_threshold_collisions_exact(tick, kernel, stats):
     """Bodies placed within +-2e-4 (relative) of every collision threshold
     (ship-ship, ship-planet, ship-bullet, bullet-planet), at tick 0 (float32
     distances) and later (float64): hit flags, rewards and bullet survival
@@ -515,7 +536,7 @@ def test_near_threshold_collisions_exact(tick, kernel):
     env.load_host(B.ships, B.ships_b, B.planets, B.bullets, B.tick, B.nplanets, B.nbullets)
     ctl = rng.randint(0, 6, size=(n, 2)).astype(np.int8)
     want, wrew, wdone = batched.step(B, ctl, P, store='f32')
-    _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False)
+    _, rew, done = env.step(torch.from_numpy(ctl).cuda(), auto_reset=False, stats=stats)
     done = done.cpu().numpy()
     assert (done == wdone).all()
     assert np.array_equal(rew.cpu().numpy(), wrew)
@@ -668,6 +689,42 @@ def test_resident_rollout_equals_stepping(kernel, case):
     assert int(done.ne(0).sum()) > 0
     if case == 'overflow_no_reset':
         assert int(((a.flags & 1) != 0).sum()) > 0   # bullets were dropped
+
+
+@pytest.mark.parametrize('kernel', ['quad', 'pair'])
+def test_resident_rollout_vs_oracle(kernel):
+    """The resident rollout (astro_rollout_res_kernel: float32 state, b_cap
+    <= 32, at most 2,048 waves, a control array -- the instance bench.py's
+    rollout line runs) on the c3 workload (3-planet filtered streams,
+    auto-reset), against the oracle directly: K = 90 ticks in ONE launch,
+    free-running numpy ticks (batched.step, float32 stores) with each
+    finished env re-created from its stream's next 3-planet seed; every
+    tick's reward and done compared, then the whole final state."""
+    from astro_amd import BatchedEnv
+    cfg = CFG['default']
+    P = batched.make_params(cfg)
+    n, K = 1000, 90
+    env = BatchedEnv(cfg, n, device='cuda:0', b_cap=32, p_pad=4, dtype=torch.float32, auto_reset=True,
+                     kernel=kernel, planets_only=3, env_offset=321)
+    env.reset()
+    seeds = batched.filtered_game_seeds(env.stream_seeds, 8, 3, cfg.max_planets, draws=220)
+    assert (env.game_seed.cpu().numpy().view(np.uint32) == seeds[:, 0]).all()
+    B = _host_batch(env)             # the oracle's start state
+    ctl = np.random.RandomState(6).randint(0, 6, size=(K, n, 2)).astype(np.int8)
+    rew, done = env.rollout(K, torch.from_numpy(ctl).cuda(), stats=False)
+    rew, done = rew.cpu().numpy(), done.cpu().numpy()
+    games = np.ones(n, np.int64)
+    for k in range(K):
+        B, wrew, wdone = batched.step(B, ctl[k], P, store='f32')
+        fin = np.nonzero(wdone)[0]
+        if fin.size:
+            B.put(fin, batched.create(seeds[fin, games[fin]], P, p_pad=4, b_cap=32, store='f32'))
+            games[fin] += 1
+        assert (done[k] == wdone).all(), k
+        assert np.array_equal(rew[k], wrew), k
+    _assert_same('resident rollout, final', _host_batch(env), B, np.ones(n, bool), rounding=True)
+    assert (env.game_seed.cpu().numpy().view(np.uint32) == seeds[np.arange(n), games - 1]).all()
+    assert games.max() > 2 and int((B.nbullets > 0).sum()) > n // 2
 
 
 PLAIN_CASES = {
