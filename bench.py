@@ -376,9 +376,10 @@ def main():
                     help="how the timed region replays a captured graph: hipGraphLaunch on its executable "
                          "graph directly (default: no per-replay wrapper; 20-step wall 14.75 -> 13.92 us median, "
                          "profiles/round3s2/ab_replay.jsonl), or torch's CUDAGraph.replay()")
-    ap.add_argument('--end-poll', default='event', choices=['event', 'stream'],
+    ap.add_argument('--end-poll', default='event', choices=['event', 'stream', 'none'],
                     help="how the host sees the region's end before its synchronize: busy-poll an event "
-                         "recorded behind the launches, or busy-poll the stream itself (no event in the region)")
+                         "recorded behind the launches, busy-poll the stream itself (no event in the region), "
+                         "or nothing (torch.cuda.synchronize alone)")
     ap.add_argument('--no-single', action='store_true', help='skip the single-game drop-in latency line')
     ap.add_argument('--stub', action='store_true', help=argparse.SUPPRESS)   # launcher test: no GPU work
     args = ap.parse_args()
@@ -526,7 +527,7 @@ def main():
             pass
     else:
         t_rec = t_sub
-        while not stream.query():
+        while args.end_poll == 'stream' and not stream.query():
             pass
     t_end = time.perf_counter()
     torch.cuda.synchronize(dev)
@@ -622,6 +623,20 @@ def main():
             ticks_per_launch=K, launches=reps, value=n * world * K * reps / wall_r, unit='env-steps/s',
             ms_per_tick=wall_r / (K * reps) * 1e3, gpu_ms_per_tick=r0.elapsed_time(r1) / (K * reps),
             policy='on-device splitmix64 random controls (bench controls stream)')
+        # the same rollouts with script.ScriptBot deciding for both ships on
+        # the device every tick (core.play's closed loop, core.py:377-410)
+        env.rollout(K, 'script', tick0=base, stats=False)
+        barrier()
+        r0.record(stream)
+        for r in range(reps):
+            env.rollout(K, 'script', tick0=base + (r + 1) * K, stats=False)
+        r1.record(stream)
+        torch.cuda.synchronize(dev)
+        barrier()
+        sms = r0.elapsed_time(r1) / (K * reps)
+        extras['rollout_script'] = dict(
+            ticks_per_launch=K, launches=reps, gpu_ms_per_tick=sms, value=n * world * 1e3 / sms,
+            unit='env-steps/s (GPU time)', policy='script.ScriptBot for every ship, decided on the device each tick')
     # (2) The observation builder (rl.ValueNetwork.get_features + to_batch):
     # an HBM-write-bound kernel; bytes = the float32 feature tensor written.
     if not args.no_features:

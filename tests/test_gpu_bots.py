@@ -128,6 +128,34 @@ def test_device_play_nothing_vs_script_matches_oracle():
     assert wins > n // 2
 
 
+@pytest.mark.parametrize('bots', ['script', ('nothing', 'script'), ('script', 'random')])
+def test_resident_scripted_rollout_equals_controls_then_step(bots):
+    """The ScriptBot instance of the resident rollout (float32 state, b_cap
+    <= 32: the state on chip for the K ticks) == K ticks of astro_controls
+    (core.Bots.control on the device, pinned above to the reference's
+    decisions) followed by astro_step with those controls, bit for bit on
+    every state array, reward and done, auto-reset included; and the random
+    ship's draws are the RANDOM policy's (global env id, tick)."""
+    from astro_amd import BatchedEnv
+    cfg = CFG['default']
+    n, K, t0 = 1200, 70, 9
+    envs = [BatchedEnv(cfg, n, device='cuda:0', b_cap=32, p_pad=4, dtype=torch.float32, auto_reset=True,
+                       kernel='pair', env_offset=40) for _ in range(2)]
+    for e in envs:
+        e.reset()
+        e.rollout(30, 'random', tick0=1 << 20)   # games of several ages first
+    a, b = envs
+    rew, done = a.rollout(K, bots, tick0=t0)
+    for k in range(K):
+        c = b.controls(bots, tick0=t0 + k)
+        _, r, d = b.step(c)
+        assert torch.equal(rew[k], r) and torch.equal(done[k], d), k
+    for f in ('ships', 'ships_b', 'planets', 'bullets', 'hdr', 'stream', 'stream_ring'):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert a.stat_dict() == b.stat_dict()
+    assert int(done.ne(0).sum()) > 0
+
+
 def test_play_bookkeeping_independent_of_chunk():
     """play's per-env game accounting (several games per env and chunk,
     games straddling chunks) does not depend on the rollout chunk length."""

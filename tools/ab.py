@@ -60,6 +60,7 @@ def main():
                                                          'ones bench.py times)')
     ap.add_argument('--stamp-rows', action='store_true', help='per-wave stats rows (for -DASTRO_STAMPS builds)')
     ap.add_argument('--burn-in', type=int, default=300, help='random-policy rollout ticks after reset (bench.py: 300)')
+    ap.add_argument('--rollout-policy', default='random', help="the rollout column's policy ('random', 'script', ...)")
     a = ap.parse_args()
     libs = a.libs.split(',')
     n = a.n_env or bench.WORKLOADS[a.workload]['n']
@@ -76,7 +77,7 @@ def main():
             torch.cuda.synchronize()
             res[lib].append(e0.elapsed_time(e1) * 1e3 / (100 * a.reps))
             e0.record()
-            env.rollout(100, 'random', tick0=1000, stats=False)
+            env.rollout(100, a.rollout_policy, tick0=1000, stats=False)
             e1.record()
             torch.cuda.synchronize()
             rolls[lib].append(e0.elapsed_time(e1) * 1e3 / 100)
@@ -85,7 +86,8 @@ def main():
         v = np.array(res[lib])
         print(json.dumps(dict(lib=lib, workload=a.workload, n=n, us_per_launch_median=float(np.median(v)),
                               us_all=[round(x, 3) for x in v],
-                              rollout_us_per_tick=float(np.median(rolls[lib])))), flush=True)
+                              rollout_us_per_tick=float(np.median(rolls[lib])), rollout_policy=a.rollout_policy)),
+              flush=True)
 
 
 if __name__ == '__main__':
