@@ -3246,9 +3246,8 @@ __device__ __forceinline__ int4 group_bcast0(const int4 &v) {   // lane 0 of the
 
 // One tick of a resident wave (quad_tick's physics, the state from R and the
 // wave's LDS rows).  ctl: this lane's control for the tick.
-template <typename T, int S, int PMAX, int LPE, bool BOTS = false>
-__device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState &st, const TickDriver &drv,
-                                         float *__restrict__ reward_all,
+template <typename T, int S, int PMAX, int LPE>
+__device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState &st, float *__restrict__ reward_all,
                                          uint8_t *__restrict__ done_all, int auto_reset, int kt, int ctl, int lane,
                                          int base, ResEnv<T, S, PMAX, LPE> &R, lds_f4 *rows,
                                          float4 (*s_body)[(S + PMAX + 1) / 2], uint32_t *s_index, int *s_kept,
@@ -3299,30 +3298,6 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
     cnt.n_pl += active && q == 0 ? uint32_t(np) : 0u;
     float rw_out = 0.0f;   // this tick's reward (lanes q < S) and done (q == 0), stored last
     uint8_t done_v = 0;
-
-    if constexpr (BOTS) {   // (the ScriptBot instance) ScriptBot ships decide on the tick's old state, as
-        // quad_tick does -- first, with broadcasts of their own, so nothing of it lives into the tick below
-        double spx[PMAX], spy[PMAX], pdx[PMAX], pdy[PMAX];
-        T mpdx[PPL], mpdy[PPL];
-#pragma unroll
-        for (int m = 0; m < PPL; ++m) {
-            mpdx[m] = pv[m].z;
-            mpdy[m] = pv[m].w;
-        }
-        bcast_slots<T, PPL, LPE>(mpx, spx);
-        bcast_slots<T, PPL, LPE>(mpy, spy);
-        bcast_slots<T, PPL, LPE>(mpdx, pdx);
-        bcast_slots<T, PPL, LPE>(mpdy, pdy);
-        const int oe = q == 0 ? S - 1 : 0;   // the other ship
-        const double ex = double(quad_bcast<0, LPE>(sv.x)), ey = double(quad_bcast<0, LPE>(sv.y));
-        const double fx = double(quad_bcast<S - 1, LPE>(sv.x)), fy = double(quad_bcast<S - 1, LPE>(sv.y));
-        const double d0x = double(quad_bcast<0, LPE>(sv.z)), d0y = double(quad_bcast<0, LPE>(sv.w));
-        const double d1x = double(quad_bcast<S - 1, LPE>(sv.z)), d1y = double(quad_bcast<S - 1, LPE>(sv.w));
-        if (q < S && ship_bot(drv, q) == ASTRO_BOT_SCRIPT)
-            ctl = script_control<S, PMAX>(drv, p.solo != 0, t0, np, spx, spy, pdx, pdy, double(sv.x), double(sv.y),
-                                          double(sv.z), double(sv.w), double(sbv), oe == 0 ? ex : fx,
-                                          oe == 0 ? ey : fy, oe == 0 ? d0x : d1x, oe == 0 ? d0y : d1y);
-    }
 
     // ---- the wave's live bullets numbered densely, first rounds read (LDS)
     const BulletsLds<S, NBOD2> bm{rows, lds_ptr(&s_body[0][0])};
@@ -3590,10 +3565,12 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
 }
 
 // Controls of the resident rollout: RANDOM / NOTHING / a control array
-// (the next tick's array entry loaded a tick ahead); BOTS: the ScriptBot
-// instance, per-ship NothingBot / ScriptBot / random decided every tick on
-// the state in registers (core.Bots.control, core.py:359-363)
-template <typename T, int S, int PMAX, int LPE, bool BOTS = false>
+// (the next tick's array entry loaded a tick ahead).  (ScriptBot policies
+// stay on quad_tick's BOTS instance: a resident ScriptBot instance, decisions
+// from the registers at each tick's start, ran 12.86-13.13 vs 12.48-12.77 us
+// per c3 tick -- the ticks are bound by the bots' arithmetic, and two bullet
+// rounds side by side spilled there; profiles/round6/ab_resident_bots.jsonl)
+template <typename T, int S, int PMAX, int LPE>
 __global__ __launch_bounds__(64 * RES_WPG, 2) void astro_rollout_res_kernel(AstroParams p, AstroState st,
                                                                            TickDriver drv,
                                                                            float *__restrict__ reward_all,
@@ -3677,7 +3654,7 @@ __global__ __launch_bounds__(64 * RES_WPG, 2) void astro_rollout_res_kernel(Astr
         } else {
             ctl = tick_control<S>(a.drv, i, sq, NN, kt);
         }
-        res_tick<T, S, PMAX, LPE, BOTS>(a.p, a.st, a.drv, a.reward, a.done, a.auto_reset, kt, ctl, lane, base, R, rows,
+        res_tick<T, S, PMAX, LPE>(a.p, a.st, a.reward, a.done, a.auto_reset, kt, ctl, lane, base, R, rows,
                                   s_body_all[wv], s_index_all[wv], s_kept_all[wv], s_hit_all[wv],
                                   s_serial_all[wv], cnt);
     }
@@ -3985,17 +3962,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         const int lpe = kind == ASTRO_KERNEL_QUAD ? 4 : 2;
         const int grid = int((int64_t(s.n_env) * lpe + QBLOCK - 1) / QBLOCK);
         const bool one = drv.ticks == 1;
-        if (drv.policy == ASTRO_POLICY_BOTS) {   // ScriptBot code lives in its own (pair) instances only
-#ifndef ASTRO_NO_RESIDENT
-            if constexpr (std::is_same<T, float>::value && PM <= 4) {   // state on chip, as the other policies
-                if (!one && p.b_cap <= RES_BCAP && int64_t(s.n_env) * 2 <= int64_t(64) * ASTRO_HELP_MAX_WAVES) {
-                    const int gr = int((int64_t(s.n_env) * 2 + 64 * RES_WPG - 1) / (64 * RES_WPG));
-                    hipLaunchKernelGGL((astro_rollout_res_kernel<T, S, PM, 2, true>), dim3(gr), dim3(64 * RES_WPG), 0,
-                                       stream, p, s, drv, r, d, st, ar);
-                    return launched("astro_rollout(pair, bots, resident)");
-                }
-            }
-#endif
+        if (drv.policy == ASTRO_POLICY_BOTS) {   // ScriptBot code lives in its own (pair) instance only
             const int g2 = int((int64_t(s.n_env) * 2 + QBLOCK - 1) / QBLOCK);
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 2, true>), dim3(g2), dim3(QBLOCK), 0, stream,
                                p, s, drv, r, d, st, ar);
@@ -4029,7 +3996,7 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
             // K ticks with the state on chip, while the grid is at most two
             // waves per SIMD (c3: 7.3 -> 7.0 us per tick; at 1M envs the
             // quad_tick instance's three waves per SIMD win: 93 vs 99 us,
-            // profiles/round5/ab_early_lazy_1m.jsonl)
+            // profiles/round5/ab_lazy_bullets_1m.jsonl)
             if (!one && p.b_cap <= RES_BCAP && int64_t(s.n_env) * lpe <= int64_t(64) * ASTRO_HELP_MAX_WAVES) {
                 const int gr = int((int64_t(s.n_env) * lpe + 64 * RES_WPG - 1) / (64 * RES_WPG));
                 if (lpe == 4)

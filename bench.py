@@ -376,10 +376,12 @@ def main():
                     help="how the timed region replays a captured graph: hipGraphLaunch on its executable "
                          "graph directly (default: no per-replay wrapper; 20-step wall 14.75 -> 13.92 us median, "
                          "profiles/round3s2/ab_replay.jsonl), or torch's CUDAGraph.replay()")
-    ap.add_argument('--end-poll', default='event', choices=['event', 'stream', 'none'],
-                    help="how the host sees the region's end before its synchronize: busy-poll an event "
-                         "recorded behind the launches, busy-poll the stream itself (no event in the region), "
-                         "or nothing (torch.cuda.synchronize alone)")
+    ap.add_argument('--end-poll', default='none', choices=['event', 'stream', 'none'],
+                    help="how the host sees the region's end before its synchronize: nothing (default: "
+                         "torch.cuda.synchronize alone, one marker round trip), busy-poll an event recorded behind "
+                         "the launches (a second marker: +0.25 us per step at 20 steps, "
+                         "profiles/round6/bench_end_poll.jsonl; the line then has the GPU span of the region), "
+                         "or busy-poll the stream itself")
     ap.add_argument('--no-single', action='store_true', help='skip the single-game drop-in latency line')
     ap.add_argument('--stub', action='store_true', help=argparse.SUPPRESS)   # launcher test: no GPU work
     args = ap.parse_args()
