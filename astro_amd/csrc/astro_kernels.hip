@@ -2439,19 +2439,24 @@ __device__ __forceinline__ void bullets_rounds(const AstroParams &p, const BM &b
           // keep the registers for occupancy instead (4 waves per SIMD with
           // no spills: c3 at 1M envs 127.5 -> 119.2 us,
           // profiles/round4/ab_1m_waves.jsonl): one at a time
-          constexpr int NR2 = PMAX <= 4 ? NRW : 1;
+          constexpr int NR2 = PMAX <= 4 ? (NRW < 2 ? NRW : 2) : 1;
+          // NRW = 3 (4 slots): a wave with a third round runs all three side by
+          // side (config 3's waves hold ~130 live bullets: half need a third)
+          constexpr bool NR3 = NRW >= 3 && PMAX <= 4;
           if (nr >= 3) {
               bws[2] = w0 + 128 + lane < wend ? s_index[128 + lane] : 0u;
               curs[2] = bm.load(bw_env(bws[2]), bw_slot(bws[2]));
           }
-          if (nr >= 2) {
+          if (NR3 && nr >= 3) {
+              rounds(std::integral_constant<int, NR3 ? 3 : 1>(), w0, bws, curs);
+          } else if (nr >= 2) {
               rounds(std::integral_constant<int, NR2>(), w0, bws, curs);
               if (NR2 == 1) rounds(std::integral_constant<int, 1>(), w0 + 64, bws + 1, curs + 1);
           } else {
               rounds(std::integral_constant<int, 1>(), w0, bws, curs);
           }
           STAMP(17);
-          if (nr >= 3) rounds(std::integral_constant<int, 1>(), w0 + 128, bws + 2, curs + 2);
+          if (!NR3 && nr >= 3) rounds(std::integral_constant<int, 1>(), w0 + 128, bws + 2, curs + 2);
           for (int r0 = w0 + 192; r0 < wend; r0 += 64) {   // uniform; rare
               const uint32_t bw = r0 + lane < wend ? s_index[r0 + lane - w0] : 0u;
               const V cur = bm.load(bw_env(bw), bw_slot(bw));
@@ -3237,6 +3242,14 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
 
 constexpr int RES_QWIN = 256;   // live bullets per LDS index window (a wave holds up to 32 x 32)
 constexpr int RES_WPG = 4;      // waves per workgroup; two workgroups per CU fit the LDS
+// bullet rounds side by side in the resident rollout (bullets_rounds NRW):
+// three when a wave has a third round (c3 100-tick rollouts 7.49 -> 7.12 us
+// per tick; in the one-tick instance with helpers three spill 4 VGPRs and
+// lose, 10.08 -> 10.30 us; profiles/round6/ab_three_rounds.jsonl)
+#ifndef ASTRO_RES_NRW
+#define ASTRO_RES_NRW 3
+#endif
+constexpr int RES_NRW = ASTRO_RES_NRW;
 
 template <int LPE>
 __device__ __forceinline__ int4 group_bcast0(const int4 &v) {   // lane 0 of the env's group to the group
@@ -3410,8 +3423,8 @@ __device__ __forceinline__ void res_tick(const AstroParams &p, const AstroState 
     }
 
     // ---- bullets (core.py:241-251, 264-266, 295-300), in the LDS rows
-    bullets_rounds<T, S, PMAX, LPE, 2, RES_QWIN>(p, bm, bin, lane, e, q, nb, sxf, syf, mpxf, mpyf, s_body, s_index,
-                                                 s_kept, s_hit, gp, gs STAMP_PASS);
+    bullets_rounds<T, S, PMAX, LPE, RES_NRW, RES_QWIN>(p, bm, bin, lane, e, q, nb, sxf, syf, mpxf, mpyf, s_body,
+                                                       s_index, s_kept, s_hit, gp, gs STAMP_PASS);
     const int wr_in = s_kept[e];
     const int hit_bits = s_hit[e];
     cnt.n_bin += active && q == 0 ? uint32_t(nb) : 0u;

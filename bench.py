@@ -322,7 +322,7 @@ def stub_rank(args, world, rank):
         print(json.dumps(out), flush=True)
 
 
-PROFILE_ROUNDS = ('round5', 'round4', 'round3', 'round2')
+PROFILE_ROUNDS = ('round6', 'round5', 'round4', 'round3', 'round2')
 ROLLOUT_LAUNCHES = 10   # the rollout line's launches at least
 
 

@@ -24,6 +24,9 @@ def main():
     ap.add_argument('--burn-in', type=int, default=300)
     ap.add_argument('--b-cap', type=int, default=0, help='override the workload\'s bullet capacity')
     ap.add_argument('--lib', default='', help='a library variant under astro_amd/ (A/B builds)')
+    ap.add_argument('--no-reset', action='store_true', help='timed rollouts without auto-reset (finished games '
+                                                            're-stepped): the reset passes\' share by difference')
+    ap.add_argument('--policy', default='random', help="the timed rollouts' policy ('random', 'script', ...)")
     a = ap.parse_args()
     if a.lib:
         from astro_amd import _lib
@@ -38,7 +41,7 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for r in range(a.launches):
-        env.rollout(a.ticks, 'random', tick0=1000 + r * a.ticks, stats=False)
+        env.rollout(a.ticks, a.policy, tick0=1000 + r * a.ticks, stats=False, auto_reset=not a.no_reset)
     e1.record()
     torch.cuda.synchronize()
     env.check_errors()
