@@ -876,6 +876,29 @@ __device__ __forceinline__ int tick_control(const TickDriver &d, int i, int s, s
 // Scalar ** 2 in the reference is pow(x, 2); x * x here (they differ only
 // where pow is not correctly rounded).
 
+// fmod(x, y) for finite x and y > 0 with |x / y| < 2^24 (float) / 2^53
+// (double), exactly, in five instructions instead of ocml's fmod: q =
+// trunc(x / y) is the true quotient's integer part or, when x / y rounded up
+// to the next integer, one more in magnitude (the division is correctly
+// rounded, so never one less); x - q y is then a multiple of y's last mantissa
+// bit smaller than y in magnitude -- exactly representable -- so the fma
+// returns it exactly, and the correction by +-y is an add whose exact result
+// (the true remainder) is representable too.  (tests/test_host.py checks the
+// argument with exact rationals.)
+template <typename C>
+__device__ __forceinline__ C exact_fmod(C x, C y) {
+    const C q = trunc(x / y);
+    C r = __builtin_fma(-q, y, x);
+    r = x >= C(0) ? (r < C(0) ? r + y : r) : (r > C(0) ? r - y : r);
+    return r;
+}
+__device__ __forceinline__ float exact_fmod(float x, float y) {
+    const float q = truncf(x / y);
+    float r = __builtin_fmaf(-q, y, x);
+    r = x >= 0.0f ? (r < 0.0f ? r + y : r) : (r > 0.0f ? r - y : r);
+    return r;
+}
+
 // util.norm_angle (util.py:125-132): ((b + pi) % (2 pi)) - pi with numpy's
 // floored remainder (npy_divmod: fmod, + divisor when the signs differ, +0
 // for a zero result), in C
@@ -884,7 +907,8 @@ __device__ __forceinline__ C np_norm_angle(C b) {
     const C pi = C(3.141592653589793);          // np.pi (float32: 3.1415927f)
     const C two_pi = C(6.283185307179586);      // 2 * np.pi
     const C x = b + pi;
-    C m = fmod(x, two_pi);
+    // (|x| < 2^24 * 2 pi: bearings change by at most dt * ship_rspeed per tick)
+    C m = exact_fmod(x, two_pi);
     m = m != C(0) ? (m < C(0) ? m + two_pi : m) : C(0);
     return m - pi;
 }

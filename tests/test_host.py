@@ -364,3 +364,34 @@ def test_gamestep_packing_without_gpu():
         return -90
     assert gs.step(ctypes.addressof(t), ctypes.cast(bad, ctypes.c_void_p).value, new, 0, 0, 0.01, 0.005, 1.0,
                    State, Bodies) == -90
+
+
+def test_exact_fmod_identity():
+    """The kernel's exact_fmod (astro_kernels.hip, used by util.norm_angle on
+    the device): q = trunc(fl(x / y)), r = fma(-q, y, x), then +-y when r
+    has the other sign than x.  With exact rationals: x - q*y is exactly
+    representable (so the fma returns it), the corrected sum is exactly
+    representable (so the add returns it), and the result is np.fmod's,
+    for float64 and float32, on random bearings and on x next to multiples
+    of 2 pi (where x / y rounds up to an integer)."""
+    from fractions import Fraction
+    rng = np.random.RandomState(7)
+    for dt in (np.float64, np.float32):
+        y = dt(6.283185307179586)
+        xs = list(rng.uniform(-3e4, 3e4, 4000).astype(dt))
+        for k in range(-400, 400):
+            m = dt(k) * y
+            xs += [np.nextafter(m, dt(np.inf)), np.nextafter(m, dt(-np.inf)), m]
+        fy = Fraction(float(y))
+        for x in xs:
+            x = dt(x)
+            q = np.trunc(dt(x / y))                           # correctly rounded division, trunc
+            exact = Fraction(float(x)) - Fraction(float(q)) * fy
+            r = dt(float(exact))
+            assert Fraction(float(r)) == exact, (dt, x)       # the fma is exact
+            if (x >= 0 and r < 0) or (x < 0 and r > 0):
+                s_exact = exact + (fy if x >= 0 else -fy)
+                r = dt(float(s_exact))
+                assert Fraction(float(r)) == s_exact, (dt, x)  # the correction is exact
+            want = np.fmod(x, y)
+            assert r == want, (dt, x, r, want)
