@@ -370,6 +370,11 @@ def main():
     ap.add_argument('--eager-head', type=int, default=0,
                     help='timed launches issued eagerly before the graph replays: the GPU runs them while the '
                          'host submits the first graph (~10-40 us), so it does not idle at the start of the region')
+    ap.add_argument('--graph-first', type=int, default=0,
+                    help='launches in the first captured graph (0 = --graph): a short first graph is '
+                         'submitted quickly, so the GPU starts while the host submits the next')
+    ap.add_argument('--host-warm-ms', type=float, default=0.0,
+                    help='busy-wait the host this long right before the clock starts (the GPU is idle then)')
     ap.add_argument('--warm-ms', type=float, default=20.0,
                     help='untimed graph replays for this long (host ms) right before the timed region')
     ap.add_argument('--replay', default='raw', choices=['torch', 'raw'],
@@ -451,7 +456,7 @@ def main():
     # the host submits the first graph.  Each graph is replayed once, untimed,
     # before the region: its first replay uploads it.
     head = min(args.steps, max(0, args.eager_head)) if args.graph > 0 else args.steps
-    graphs, replays = [], []
+    graphs, replays, graph_sizes = [], [], []
     use_c = args.launcher == 'c'
     if use_c:   # the K launches issued from C (astro_step_many), per-tick outputs
         head = 0
@@ -461,10 +466,17 @@ def main():
         cap = torch.cuda.Stream(dev)
         cap.wait_stream(stream)
         with torch.cuda.stream(cap):
-            for g0 in range(head, args.steps, args.graph):
+            bounds, g0 = [], head
+            if args.graph_first > 0 and g0 < args.steps:   # a short first graph: submitted quickly
+                bounds.append((g0, min(args.steps, g0 + args.graph_first)))
+                g0 = bounds[-1][1]
+            for g1 in range(g0, args.steps, args.graph):
+                bounds.append((g1, min(args.steps, g1 + args.graph)))
+            graph_sizes[:] = [b1 - b0 for b0, b1 in bounds]
+            for b0, b1 in bounds:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cap):
-                    for k in range(g0, min(args.steps, g0 + args.graph)):
+                    for k in range(b0, b1):
                         env.launch(ptrs[args.warmup + k], stats=cnt)
                 graphs.append(g)
         stream.wait_stream(cap)
@@ -514,6 +526,10 @@ def main():
     poll_event = args.end_poll == 'event'
     if poll_event:   # (instrumentation, before the clock starts: the GPU is idle, it runs at once)
         ev0.record(stream)
+    if args.host_warm_ms > 0:   # (host only: the CPU core busy before the clock starts, the GPU idle)
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < args.host_warm_ms * 1e-3:
+            pass
     t0 = time.perf_counter()
     if use_c:
         env.launch_many(ptrs[args.warmup], args.steps, rew_k.data_ptr(), done_k.data_ptr(), stats=cnt)
@@ -760,9 +776,9 @@ def main():
                       'stats buffer does): the stats below and the section 8(d) bytes per launch' % args.steps),
             timed_region=('%d launches issued from C in one astro_step_many call' % args.steps) if use_c else
                          '%d launches: %d eager, then %s' % (
-                args.steps, head, ('%d hipGraph replay(s) of up to %d launches (%s), each graph replayed once '
+                args.steps, head, ('%d hipGraph replay(s) of %s launches (%s), each graph replayed once '
                                    'untimed before the region' % (
-                                       len(graphs), args.graph,
+                                       len(graphs), '+'.join(str(x) for x in graph_sizes),
                                        'hipGraphLaunch' if args.replay == 'raw' else 'torch CUDAGraph.replay'))
                 if graphs else 'no graph'),
             dist=dict(initialized=dist_on, backend=backend if dist_on else None, world=world,
