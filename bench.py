@@ -504,6 +504,14 @@ def main():
             replays = [raw(g.raw_cuda_graph_exec()) for g in graphs]
         for r in replays:   # (the first replay uploads the graph)
             r()
+        if not cnt:
+            # the statistics at the region's start, read BEFORE the warm
+            # replays: the launches they and the region run leave the stats
+            # rows alone, and the region then follows the warm replays with
+            # nothing but a synchronize in between (no reduction kernels or
+            # copies: the same-process region A/B, tools/region_ab.py, times
+            # 10.6-10.7 us per step back to back; after the stats read 11.2+)
+            s0 = env.stat_dict()
         # keep the GPU busy for --warm-ms before the region, continuing the
         # games with the same graphs: on a box that idled before this process
         # the first short region ran at 20 us per step on the GPU's own
@@ -519,8 +527,9 @@ def main():
             ev_w.record(stream)
             while not ev_w.query():
                 pass
-    barrier()
-    s0 = env.stat_dict()
+    if cnt or not graphs:
+        barrier()
+        s0 = env.stat_dict()
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     poll_event = args.end_poll == 'event'
