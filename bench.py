@@ -432,11 +432,19 @@ def main():
     ptrs = [ctl[t].data_ptr() for t in range(ticks)]
     stream = torch.cuda.current_stream(dev)
 
+    # the ranks' rendezvous: a host-side (gloo) group next to RCCL's, so a
+    # barrier puts no collective kernel on the GPU right before the timed
+    # region (the region follows the warm replays with nothing else between)
+    bar_group = None
+    if dist_on and backend == 'nccl':
+        import torch.distributed as dist
+        bar_group = dist.new_group(backend='gloo')
+
     def barrier():
         torch.cuda.synchronize(dev)
         if dist_on:
             import torch.distributed as dist
-            dist.barrier()
+            dist.barrier(group=bar_group)
 
     # settle: a few eager launches of the one-tick instance after the burn-in's
     # rollout instance (the first launch after the switch is the slow one),
@@ -791,6 +799,8 @@ def main():
                                        'hipGraphLaunch' if args.replay == 'raw' else 'torch CUDAGraph.replay'))
                 if graphs else 'no graph'),
             dist=dict(initialized=dist_on, backend=backend if dist_on else None, world=world,
+                      barrier=('host-side gloo group' if bar_group is not None else
+                               (backend if dist_on else None)),
                       reductions='device tensors (RCCL all_reduce)' if dist_on and red_dev is not None
                       else ('host tensors (gloo)' if dist_on else 'none (one rank)')),
             burn_in_ticks=args.burn_in, settle_launches=settle, warm_ms=args.warm_ms,

@@ -41,7 +41,7 @@ def test_bench_rank_over_rccl_at_world_size_one():
     lines = [l for l in p.stdout.splitlines() if l.strip().startswith('{')]
     assert len(lines) == 1, p.stdout
     j = json.loads(lines[0])
-    assert j['dist'] == dict(initialized=True, backend='nccl', world=1,
+    assert j['dist'] == dict(initialized=True, backend='nccl', world=1, barrier='host-side gloo group',
                              reductions='device tensors (RCCL all_reduce)')
     assert j['ranks'] == 1 and j['n_gpus'] == 1 and j['value'] > 0
     agg = j['roofline']['aggregate']
