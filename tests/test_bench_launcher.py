@@ -85,3 +85,20 @@ def test_counting_pass_skipped_on_device_errors():
     s0, s1 = {'resets': 1}, {'resets': 5}
     out = bench.counting_pass(FakeEnv(), launched.append, 20, s0, s1, 0x4, 0.0101)
     assert out == (s0, s1, 0.0101, 0x4) and launched == []
+
+
+def test_region_breakdown_names_the_host_share():
+    """bench.py's region_host_us: the host timestamps of the timed region,
+    the launches' back-to-back GPU time, and -- when the event pair around
+    the region was recorded -- the GPU's idle time inside it and the host's
+    time after it."""
+    sys.path.insert(0, ROOT)
+    import bench
+    st = dict(submitted=12.0, end_event_recorded=12.0, end_seen=12.5, synchronized=212.0)
+    r = bench.region_breakdown(st, None, 0.0099, 20)
+    assert abs(r['kernels_back_to_back'] - 198.0) < 1e-9
+    assert abs(r['wall_minus_kernels_per_step'] - 0.7) < 1e-9
+    assert 'gpu_span_events' not in r
+    r = bench.region_breakdown(st, 0.0102, 0.0099, 20)
+    assert abs(r['gpu_span_events'] - 204.0) < 1e-9 and abs(r['gpu_idle_in_span'] - 6.0) < 1e-9
+    assert abs(r['host_after_gpu_span'] - 8.0) < 1e-9
