@@ -202,7 +202,7 @@ class _Shim:
             t.out = self.outbuf.__array_interface__['data'][0]
             # the caller's current stream, refreshed on every tick (step)
             self.dev_index = env.device.index if env.device.index is not None else torch.cuda.current_device()
-            t.stream = torch._C._cuda_getCurrentRawStream(self.dev_index)
+            t.stream = _raw_stream(self.dev_index)
             self.tick = t
             self.tick_ptr = ctypes.addressof(t)
             self.game_step = env.lib.astro_game_step
@@ -249,7 +249,9 @@ _LAST = (None, None, None, None)
 _SHIM_LOCK = threading.Lock()
 
 
-_raw_stream = torch._C._cuda_getCurrentRawStream   # (device index -> hipStream_t, ~0.1 us)
+# device index -> the current hipStream_t (~0.1 us; torch's public path as a fallback)
+_raw_stream = getattr(torch._C, '_cuda_getCurrentRawStream', None) or (
+    lambda d: torch.cuda.current_stream(d).cuda_stream)
 
 
 def _shim(config, bullets_needed):

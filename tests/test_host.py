@@ -395,3 +395,22 @@ def test_exact_fmod_identity():
                 assert Fraction(float(r)) == s_exact, (dt, x)  # the correction is exact
             want = np.fmod(x, y)
             assert r == want, (dt, x, r, want)
+
+
+def test_shim_cache_clear_drops_the_fast_path():
+    """Emptying the single-game shim cache (clear_shims, or any clear/pop/
+    del on it) also drops the per-tick fast path (_LAST), so a cleared
+    shim's arena is never used again."""
+    from astro_amd import core
+    saved = dict(core._ENVS)
+    try:
+        for drop in (lambda c: c.clear(), lambda c: c.pop('k'), lambda c: c.__delitem__('k'), lambda c: c.popitem()):
+            core._ENVS['k'] = object()
+            core._LAST = ('cfg', 0, object(), core._ENVS)
+            drop(core._ENVS)
+            assert core._LAST == (None, None, None, None)
+        core._LAST = ('cfg', 0, object(), core._ENVS)
+        core.clear_shims()
+        assert core._LAST == (None, None, None, None) and not core._ENVS
+    finally:
+        core._ENVS.update(saved)
