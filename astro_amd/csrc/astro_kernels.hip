@@ -3815,7 +3815,10 @@ __global__ __launch_bounds__(FEAT_BLOCK) void astro_features_kernel(AstroParams 
     const float *src = reinterpret_cast<const float *>(s_out);
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         const int64_t n4 = nf / 4;
-        for (int64_t k = t; k < n4; k += FEAT_BLOCK) reinterpret_cast<float4 *>(dst)[k] = s_out[k];
+        // (nontemporal: the tensor is written once and read by the caller
+        // later; 27.6-28.0 -> 25.9-26.2 us for [65,536, 36, 15],
+        // profiles/round6/ab_features_nt.txt)
+        for (int64_t k = t; k < n4; k += FEAT_BLOCK) st_out(reinterpret_cast<float4 *>(dst) + k, s_out[k]);
         for (int64_t k = n4 * 4 + t; k < nf; k += FEAT_BLOCK) dst[k] = src[k];
     } else {
         for (int64_t k = t; k < nf; k += FEAT_BLOCK) dst[k] = src[k];
