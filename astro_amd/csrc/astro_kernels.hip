@@ -2520,7 +2520,18 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // of c2 lost with it there: 5.08 -> 5.33 us, ab_quad_planets_on_helper.jsonl)
     constexpr bool PLANETS_ON_HELPER = HELP && LPE == 2;
     const bool helper = HELP && int(threadIdx.x >> 6) >= WPG;
-    const int wv = WPG == 1 ? 0 : int(threadIdx.x >> 6) - (helper ? WPG : 0);   // (a helper: its step wave's)
+    // Helper wave WPG + h serves step wave (h + 1) mod WPG: a workgroup's waves
+    // go round the 4 SIMDs in order, so a helper would otherwise share its
+    // SIMD with its own step wave, and the two are each other's competition
+    // at the launch's end (a late post: the step wave's stores and its
+    // helper's reset pass).  c3 10.17 -> 10.08 us, c2 unchanged
+    // (profiles/round6/ab_helper_simd.jsonl)
+#ifndef ASTRO_HELPER_SHIFT
+#define ASTRO_HELPER_SHIFT 1
+#endif
+    const int wv = WPG == 1 ? 0
+                            : (helper ? (int(threadIdx.x >> 6) - WPG + ASTRO_HELPER_SHIFT) % WPG
+                                      : int(threadIdx.x >> 6));   // (a helper: its step wave's)
     float4 (*s_body)[NBOD2] = s_body_all[wv];
     uint32_t *s_index = s_index_all[wv];
     int *s_kept = s_kept_all[wv], *s_hit = s_hit_all[wv], *s_serial = s_serial_all[wv];
