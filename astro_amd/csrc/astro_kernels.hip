@@ -2529,6 +2529,19 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
 #ifndef ASTRO_HELPER_SHIFT
 #define ASTRO_HELPER_SHIFT 1
 #endif
+    // Wave priorities (s_setprio), pair instance: step waves 2 until their
+    // post, then 0; helpers 1.  After its post a step wave's work (fire, own
+    // ship, header) ends nothing but itself, while the helpers' reset passes
+    // end the launch: c3 10.13 -> 9.74 us (the digits of ASTRO_PRIO: step
+    // wave before / after the post, helper before / after; 2011 kept, 1011
+    // 9.78, 3021 9.74, 2012 9.98, 1000 10.13, 1001 10.21; the quad instance
+    // of c2 lost with 1011, 4.09 -> 4.24: profiles/round6/ab_wave_priority.jsonl)
+#ifndef ASTRO_PRIO
+#define ASTRO_PRIO 2011
+#endif
+    constexpr bool PRIO = HELP && LPE == 2 && ASTRO_PRIO != 0;
+    constexpr int PRIO_SP = (ASTRO_PRIO / 1000) % 10, PRIO_SQ = (ASTRO_PRIO / 100) % 10;
+    constexpr int PRIO_HP = (ASTRO_PRIO / 10) % 10, PRIO_HQ = ASTRO_PRIO % 10;
     const int wv = WPG == 1 ? 0
                             : (helper ? (int(threadIdx.x >> 6) - WPG + ASTRO_HELPER_SHIFT) % WPG
                                       : int(threadIdx.x >> 6));   // (a helper: its step wave's)
@@ -2559,6 +2572,10 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
         }
         __syncthreads();
         if (base >= N) return QuadCounts{};
+        if constexpr (PRIO) {
+            if (helper) __builtin_amdgcn_s_setprio(PRIO_HP);
+            else __builtin_amdgcn_s_setprio(PRIO_SP);
+        }
         if (helper) {
             HSTAMP_R(23);
             HSTAMP_T(24);
@@ -2659,6 +2676,13 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 return QuadCounts{};
             }
             asm volatile("" ::: "memory");
+#ifdef ASTRO_PRIO_DYN
+            if (PRIO && (ASTRO_PRIO_DYN & 2)) {
+                if (bx.todo) __builtin_amdgcn_s_setprio(PRIO_HQ);
+                else __builtin_amdgcn_s_setprio(0);
+            } else
+#endif
+            if constexpr (PRIO && PRIO_HQ != PRIO_HP) __builtin_amdgcn_s_setprio(PRIO_HQ);
             HSTAMP_R(20);
             HSTAMP_T(27);
             QuadCounts hc{};
@@ -2797,6 +2821,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const BulletsIn<T> bin =
         bullets_begin<T, LPE, QWIN, EAGER_BULLETS>(bgl, lane, e, q, nb, np, t0, s_index, s_kept, s_hit, s_serial);
     const int total = bin.total;
+#ifdef ASTRO_PRIO_DYN
+    if (PRIO && (ASTRO_PRIO_DYN & 1) && total > ASTRO_PRIO_DYN_B) __builtin_amdgcn_s_setprio(PRIO_SP + 1);   // uniform
+#endif
     STAMP(19);
     // key[397] of the next game's seed (first step of a game): a random
     // gather into the 4 GiB key table, issued after every load the physics
@@ -2991,6 +3018,7 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
             // (lane 0 is active in every wave that gets here: base < N)
             if (!EARLY_POST || total > 0)   // uniform (a wave without bullets posted before its bullet pass)
                 help_post(s_box_all[wv], __ballot(done && auto_reset && q == 0), lane);
+            if constexpr (PRIO && PRIO_SQ != PRIO_SP) __builtin_amdgcn_s_setprio(PRIO_SQ);
         }
 
         if (!done) {   // uniform over the quad
