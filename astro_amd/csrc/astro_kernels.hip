@@ -2535,7 +2535,9 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     // end the launch: c3 10.13 -> 9.74 us (the digits of ASTRO_PRIO: step
     // wave before / after the post, helper before / after; 2011 kept, 1011
     // 9.78, 3021 9.74, 2012 9.98, 1000 10.13, 1001 10.21; the quad instance
-    // of c2 lost with 1011, 4.09 -> 4.24: profiles/round6/ab_wave_priority.jsonl)
+    // of c2 lost with 1011, 4.09 -> 4.24; priorities from the wave's live
+    // bullets, or for helpers with resets only, were even or slower:
+    // profiles/round6/ab_wave_priority.jsonl)
 #ifndef ASTRO_PRIO
 #define ASTRO_PRIO 2011
 #endif
@@ -2676,12 +2678,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
                 return QuadCounts{};
             }
             asm volatile("" ::: "memory");
-#ifdef ASTRO_PRIO_DYN
-            if (PRIO && (ASTRO_PRIO_DYN & 2)) {
-                if (bx.todo) __builtin_amdgcn_s_setprio(PRIO_HQ);
-                else __builtin_amdgcn_s_setprio(0);
-            } else
-#endif
             if constexpr (PRIO && PRIO_HQ != PRIO_HP) __builtin_amdgcn_s_setprio(PRIO_HQ);
             HSTAMP_R(20);
             HSTAMP_T(27);
@@ -2821,9 +2817,6 @@ __device__ __forceinline__ QuadCounts quad_tick(const AstroParams &p, const Astr
     const BulletsIn<T> bin =
         bullets_begin<T, LPE, QWIN, EAGER_BULLETS>(bgl, lane, e, q, nb, np, t0, s_index, s_kept, s_hit, s_serial);
     const int total = bin.total;
-#ifdef ASTRO_PRIO_DYN
-    if (PRIO && (ASTRO_PRIO_DYN & 1) && total > ASTRO_PRIO_DYN_B) __builtin_amdgcn_s_setprio(PRIO_SP + 1);   // uniform
-#endif
     STAMP(19);
     // key[397] of the next game's seed (first step of a game): a random
     // gather into the 4 GiB key table, issued after every load the physics
