@@ -43,7 +43,10 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "astro_step.h"
 
@@ -840,6 +843,7 @@ struct TickDriver {
     double script_r2, script_threshold, ship_thrust, ship_rspeed, bullet_speed, ship_radius;
     uint32_t *flag;          // astro_game_step: the completion word the one wave stores flag_seq to
     uint32_t flag_seq;
+    int32_t late_block;      // > 0: blocks from here on are the grid's last, partial round (late_block_of)
 };
 
 __device__ __forceinline__ int ship_bot(const TickDriver &d, int s) {
@@ -3240,7 +3244,15 @@ __global__ __launch_bounds__(HELP ? 2 * (64 * WPG) : (64 * WPG), MULTI ? (BOTS |
     //      but the tick number lives across the loop
     // (HELP: waves WPG.. are the helpers of waves 0..WPG-1, same stats row)
     if (!HELP && int(blockIdx.x * WPG + threadIdx.x / 64) * (64 / LPE) >= st.n_env) return;   // a spare wave of the last block
-    // (HELP: a spare wave returns inside quad_tick, after the workgroup's one barrier)
+    // (HELP: a spare wave returns inside quad_tick, after the workgroup's one
+    // barrier)  A one-tick grid larger than the device holds at once runs in
+    // rounds; the blocks of its last, partial round start last and end the
+    // launch, so they run at a higher priority than the previous round's
+    // stragglers (c5: 1.33 rounds, 28.15 -> 26.97 us; the last quarter of the
+    // grid measured: profiles/round6/ab_late_round_priority.jsonl)
+    if constexpr (!MULTI && !HELP) {
+        if (drv.late_block > 0 && int(blockIdx.x) >= drv.late_block) __builtin_amdgcn_s_setprio(1);
+    }
     const int n_ticks = MULTI ? drv.ticks : 1;   // (astro_step: a one-tick instance without the loop)
     for (int kt = 0; kt < n_ticks; ++kt) {
         QuadCounts c;
@@ -4019,6 +4031,32 @@ int pick_kernel(const AstroParams &p, int n_env) {
     return n_env <= ASTRO_QUAD_MAX_ENVS ? ASTRO_KERNEL_QUAD : ASTRO_KERNEL_PAIR;
 }
 
+// The first block of a grid's last, partial round: blocks the device holds
+// at once = blocks per CU at this kernel's occupancy x CUs (cached per
+// kernel and device); 0 when the grid runs in one round or in whole rounds
+__host__ inline int late_block_of(const void *fn, int block, int grid) {
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    int cap = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        const auto key = std::make_pair(fn, dev);
+        const auto it = cache.find(key);
+        if (it != cache.end()) {
+            cap = it->second;
+        } else {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, 0) != hipSuccess) per_cu = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+            cap = per_cu * cus;
+            cache[key] = cap;
+        }
+    }
+    return cap > 0 && grid > cap && grid % cap != 0 ? (grid / cap) * cap : 0;
+}
+
 template <typename T, int S, int PM>
 int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv, float *r, uint8_t *d,
                 uint64_t *stats, int ar, hipStream_t stream) {
@@ -4095,12 +4133,20 @@ int launch_step(const AstroParams &p, const AstroState &s, const TickDriver &drv
         else if (one) {
             constexpr int W = PM > 4 ? QW : QW_PAIR;
             const dim3 g(int((int64_t(s.n_env) * 2 + 64 * W - 1) / (64 * W))), b(64 * W);
-            if (count)
+            TickDriver dl = drv;
+            if (count) {
+                dl.late_block = late_block_of(
+                    reinterpret_cast<const void *>(&astro_step_quad_kernel<T, S, PM, false, 2, false, false, W, true>),
+                    int(b.x), int(g.x));
                 hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, false, W, true>), g, b, 0, stream,
-                                   p, s, drv, r, d, st, ar);
-            else
+                                   p, s, dl, r, d, st, ar);
+            } else {
+                dl.late_block = late_block_of(
+                    reinterpret_cast<const void *>(&astro_step_quad_kernel<T, S, PM, false, 2, false, false, W, false>),
+                    int(b.x), int(g.x));
                 hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, false, 2, false, false, W, false>), g, b, 0,
-                                   stream, p, s, drv, r, d, st, ar);
+                                   stream, p, s, dl, r, d, st, ar);
+            }
         }
         else
             hipLaunchKernelGGL((astro_step_quad_kernel<T, S, PM, true, 2>), dim3(grid), dim3(QBLOCK), 0, stream, p,
